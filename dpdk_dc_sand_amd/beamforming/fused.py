@@ -1,0 +1,102 @@
+"""One-pass beamformer: reorder + per-batch coefficient regeneration + multiply (MI355X-native operator).
+
+The reference's OpSequence (beamform_op_sequence.py:117-157) makes three passes: the reorder reads and
+writes the whole voltage cube (prebeamform_reorder_kernel.mako:37-93), the coefficient generator writes a
+(B, P, C, 2A, 2M) f32 table replicated over batches and pols (16 B per complex coefficient, as large as the
+voltages at 16 beams), and the multiply reads both back.  `FusedBeamformer` reads the raw (B, A, C, T, 2, 2)
+cube once, generates each (b, c)'s coefficients in-kernel from the delay model (float64 phase, the same
+arithmetic as CoeffGenerator, so with zero rates the output equals OpSequence's), and writes the beams once:
+the HBM traffic is the algorithmic minimum.
+
+Per-block regeneration (BeamformerParameters.h:17 ACCUMULATIONS_BEFORE_NEW_COEFFS, the C++ study's
+time-dependent kernels BeamformerKernels.cu:121-189 and the fused study kernel :192-367): batch b is steered
+at dt_b = t0 + b * batch_dt using the delay and phase rates (SURVEY A3 convention).
+"""
+import numpy as np
+
+from .. import _lib, accel
+
+
+class FusedBeamformerTemplate:
+    """Template for the fused beamformer.
+
+    Parameters
+    ----------
+    context, n_batches, n_channels_per_stream, n_channels (whole band), n_samples_per_channel, n_ants, n_beams,
+    xeng_id, sample_period -- as the reference templates.
+    delay_channels: 1 (one delay model for every channel, the physical case; 16*A*M bytes) or
+        n_channels_per_stream (the reference's per-channel (C, M, A, 4) table).  Default: n_channels_per_stream.
+    sample_signed: read voltages as int8 instead of uint8.
+    out_int8, out_scale: write int8 beams sat127(rne(y * out_scale)) instead of float32.
+    t0, batch_dt: steering time of batch 0 and the step between batches (seconds).
+    """
+
+    def __init__(self, context, n_batches: int, n_channels_per_stream: int, n_channels: int,
+                 n_samples_per_channel: int, n_ants: int, n_beams: int, xeng_id: int = 0,
+                 sample_period: float = 1 / 1712e6, delay_channels=None, sample_signed: bool = False,
+                 out_int8: bool = False, out_scale: float = 1.0, t0: float = 0.0, batch_dt: float = 0.0) -> None:
+        for name, v in dict(n_batches=n_batches, n_channels_per_stream=n_channels_per_stream, n_channels=n_channels,
+                            n_samples_per_channel=n_samples_per_channel, n_ants=n_ants, n_beams=n_beams).items():
+            if int(v) <= 0:
+                raise ValueError(f"{name} must be positive, got {v}")
+        if n_samples_per_channel % 16:
+            raise ValueError("n_samples_per_channel must be a multiple of 16")
+        if delay_channels is None:
+            delay_channels = n_channels_per_stream
+        if delay_channels not in (1, n_channels_per_stream):
+            raise ValueError("delay_channels must be 1 or n_channels_per_stream")
+        if not sample_period > 0:
+            raise ValueError("sample_period must be > 0")
+        self.context = context
+        self.n_batches = n_batches
+        self.n_pols = 2
+        self.n_channels_per_stream = n_channels_per_stream
+        self.n_channels = n_channels
+        self.n_samples_per_channel = n_samples_per_channel
+        self.n_samples_per_block = 16
+        self.n_blocks = n_samples_per_channel // 16
+        self.n_ants = n_ants
+        self.n_beams = n_beams
+        self.xeng_id = xeng_id
+        self.sample_period = sample_period
+        self.delay_channels = delay_channels
+        self.sample_signed = bool(sample_signed)
+        self.out_int8 = bool(out_int8)
+        self.out_scale = float(out_scale)
+        self.t0 = float(t0)
+        self.batch_dt = float(batch_dt)
+        B, C, T, A, M = n_batches, n_channels_per_stream, n_samples_per_channel, n_ants, n_beams
+        self.input_shape = (B, A, C, T, 2, 2)
+        self.delay_shape = (delay_channels, M, A, 4)
+        self.output_shape = (B, 2, C, T // 16, 16, 2 * M)
+
+    def algorithmic_bytes(self):
+        """HBM bytes one launch must move: voltages once, beams once, delay model once."""
+        return _lib.load().bf_fused_algorithmic_bytes(self.n_batches, self.n_channels_per_stream,
+                                                      self.n_samples_per_channel, self.n_ants, self.n_beams,
+                                                      self.delay_channels, int(self.out_int8))
+
+    def instantiate(self, command_queue):
+        return FusedBeamformer(self, command_queue)
+
+
+class FusedBeamformer(accel.Operation):
+    """.. rubric:: Slots
+    inSamples: (n_batches, n_ants, n_channels_per_stream, n_samples_per_channel, 2, 2), uint8 (int8 if signed)
+    delay_vals: (delay_channels, n_beams, n_ants, 4), float32
+    outData: (n_batches, 2, n_channels_per_stream, n_blocks, 16, 2*n_beams), float32 (int8 if out_int8)
+    """
+
+    def __init__(self, template: FusedBeamformerTemplate, command_queue):
+        super().__init__(command_queue)
+        self.template = t = template
+        self.slots["inSamples"] = accel.IOSlot(t.input_shape, np.int8 if t.sample_signed else np.uint8)
+        self.slots["delay_vals"] = accel.IOSlot(t.delay_shape, np.float32)
+        self.slots["outData"] = accel.IOSlot(t.output_shape, np.int8 if t.out_int8 else np.float32)
+
+    def _run(self):
+        t = self.template
+        _lib.call("bf_beamform_fused", self.buffer("inSamples").ptr, self.buffer("delay_vals").ptr, t.delay_channels,
+                  self.buffer("outData").ptr, t.n_batches, t.n_channels_per_stream, t.n_samples_per_channel,
+                  t.n_ants, t.n_beams, t.n_channels, t.xeng_id, float(t.sample_period), t.t0, t.batch_dt,
+                  int(t.sample_signed), int(t.out_int8), t.out_scale, self.command_queue.handle)

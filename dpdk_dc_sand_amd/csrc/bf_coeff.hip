@@ -1,0 +1,113 @@
+// Steering-coefficient generators.
+//
+// bf_coeff_gen      -- Python layout (B, P, C, 2A, 2M) f32, bit-exact to CoeffGenerator.cpu_coeffs
+//                      (unit_test/coeff_generator_cpu.py:78-187); replaces run_coeff_gen
+//                      (beamforming/coeff_generator.py:12-103) without its ant/beam transposition.
+// bf_coeff_gen_time -- compact time-dependent form (n_times, C, A, M) complex f32 or f16, the C++ study's
+//                      grouped_channels_and_timestamps / b16BitOutput modes (BeamformerKernels.cu:121-189)
+//                      with the Python sign convention.
+//
+// Work is C*A*M phasors (tiny next to the beamform); the kernels are write-bound.  One thread per (c, a, m),
+// m fastest, so the (cos, sin) / (-sin, cos) float2 pairs of consecutive threads are contiguous in a row of
+// the 2M-wide output.
+#include <hip/hip_fp16.h>
+
+#include "bf_common.hpp"
+#include "bf_phase.hpp"
+
+namespace bf {
+
+__global__ __launch_bounds__(256) void coeff_gen_kernel(const float4* __restrict__ dv, float* __restrict__ out,
+                                                        int B, int P, int C, int A, int M, long long base_ch,
+                                                        double ctot, double ts) {
+  const long long n = static_cast<long long>(C) * A * M;
+  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+  const size_t plane = static_cast<size_t>(2 * A) * (2 * M);  // one (b, p, c) coefficient matrix
+  for (long long idx = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < n; idx += stride) {
+    const int m = static_cast<int>(idx % M);
+    const int a = static_cast<int>((idx / M) % A);
+    const int c = static_cast<int>(idx / (static_cast<long long>(M) * A));
+    const float4 d = dv[(static_cast<size_t>(c) * M + m) * A + a];  // delay_vals[c][m][a]
+    float re, im;
+    steering_coeff(d, static_cast<double>(base_ch + c), ctot, ts, 0.0, &re, &im);
+    const float2 row0 = make_float2(re, im);   // W[2a][2m], W[2a][2m+1]
+    const float2 row1 = make_float2(-im, re);  // W[2a+1][2m], W[2a+1][2m+1]
+    for (int bp = 0; bp < B * P; ++bp) {
+      float* w = out + (static_cast<size_t>(bp) * C + c) * plane;
+      *reinterpret_cast<float2*>(w + static_cast<size_t>(2 * a) * (2 * M) + 2 * m) = row0;
+      *reinterpret_cast<float2*>(w + static_cast<size_t>(2 * a + 1) * (2 * M) + 2 * m) = row1;
+    }
+  }
+}
+
+template <bool F16>
+__global__ __launch_bounds__(256) void coeff_gen_time_kernel(const float4* __restrict__ dv, int delay_channels,
+                                                             void* __restrict__ out, int n_times, int C, int A, int M,
+                                                             long long base_ch, double ctot, double ts, double t0,
+                                                             double dt_step) {
+  const long long n = static_cast<long long>(n_times) * C * A * M;
+  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+  for (long long idx = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < n; idx += stride) {
+    const int m = static_cast<int>(idx % M);
+    long long r = idx / M;
+    const int a = static_cast<int>(r % A);
+    r /= A;
+    const int c = static_cast<int>(r % C);
+    const int t = static_cast<int>(r / C);
+    const int cd = delay_channels == 1 ? 0 : c;
+    const float4 d = dv[(static_cast<size_t>(cd) * M + m) * A + a];
+    float re, im;
+    steering_coeff(d, static_cast<double>(base_ch + c), ctot, ts, t0 + t * dt_step, &re, &im);
+    if constexpr (F16) {
+      reinterpret_cast<__half2*>(out)[idx] = __floats2half2_rn(re, im);
+    } else {
+      reinterpret_cast<float2*>(out)[idx] = make_float2(re, im);
+    }
+  }
+}
+
+static int grid_for(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 256LL * 16) g = 256LL * 16;  // grid-stride beyond 16 blocks per CU
+  return static_cast<int>(g < 1 ? 1 : g);
+}
+
+}  // namespace bf
+
+extern "C" int bf_coeff_gen(const float* delay_vals, float* out, int B, int P, int C, int Ctot, int A, int M,
+                            int xeng_id, double sample_period, void* stream) {
+  BF_REQUIRE(delay_vals && out, "bf_coeff_gen: null pointer");
+  BF_REQUIRE(B > 0 && P > 0 && C > 0 && A > 0 && M > 0 && Ctot > 0 && xeng_id >= 0,
+             "bf_coeff_gen: bad shape B=%d P=%d C=%d A=%d M=%d Ctot=%d xeng_id=%d", B, P, C, A, M, Ctot, xeng_id);
+  BF_REQUIRE(sample_period > 0.0, "bf_coeff_gen: sample_period must be > 0");
+  BF_REQUIRE((reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0,
+             "bf_coeff_gen: misaligned buffer");
+  const long long n = static_cast<long long>(C) * A * M;
+  hipLaunchKernelGGL(bf::coeff_gen_kernel, dim3(bf::grid_for(n)), dim3(256), 0, bf::as_stream(stream),
+                     reinterpret_cast<const float4*>(delay_vals), out, B, P, C, A, M,
+                     static_cast<long long>(C) * xeng_id, static_cast<double>(Ctot), sample_period);
+  BF_LAUNCHED("coeff_gen_kernel");
+}
+
+extern "C" int bf_coeff_gen_time(const float* delay_vals, int delay_channels, void* out, int out_fp16,
+                                 int n_times, int C, int Ctot, int A, int M, int xeng_id, double sample_period,
+                                 double t0, double dt_step, void* stream) {
+  BF_REQUIRE(delay_vals && out, "bf_coeff_gen_time: null pointer");
+  BF_REQUIRE(n_times > 0 && C > 0 && A > 0 && M > 0 && Ctot > 0 && xeng_id >= 0,
+             "bf_coeff_gen_time: bad shape");
+  BF_REQUIRE(delay_channels == 1 || delay_channels == C, "bf_coeff_gen_time: delay_channels must be 1 or C");
+  BF_REQUIRE(sample_period > 0.0, "bf_coeff_gen_time: sample_period must be > 0");
+  const long long n = static_cast<long long>(n_times) * C * A * M;
+  const auto dv = reinterpret_cast<const float4*>(delay_vals);
+  const long long base = static_cast<long long>(C) * xeng_id;
+  if (out_fp16) {
+    hipLaunchKernelGGL(bf::coeff_gen_time_kernel<true>, dim3(bf::grid_for(n)), dim3(256), 0, bf::as_stream(stream),
+                       dv, delay_channels, out, n_times, C, A, M, base, static_cast<double>(Ctot), sample_period, t0,
+                       dt_step);
+  } else {
+    hipLaunchKernelGGL(bf::coeff_gen_time_kernel<false>, dim3(bf::grid_for(n)), dim3(256), 0,
+                       bf::as_stream(stream), dv, delay_channels, out, n_times, C, A, M, base,
+                       static_cast<double>(Ctot), sample_period, t0, dt_step);
+  }
+  BF_LAUNCHED("coeff_gen_time_kernel");
+}

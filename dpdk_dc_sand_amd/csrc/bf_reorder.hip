@@ -1,0 +1,87 @@
+// Pre-beamform reorder: u16 (B, A, C, T, P) -> (B, P, C, T/16, 16, A), bit-exact.
+// Replaces the mako/PyCUDA kernel prebeamform_reorder (beamforming/kernels/prebeamform_reorder_kernel.mako:37-93),
+// contract = beamforming/reorder.py:40-42.
+//
+// The reference kernel moves one u16 per thread with A-strided scattered stores.  Here one workgroup owns a
+// (b, c, time-chunk) tile: every antenna's contiguous run of TT*4 bytes is loaded with 16-byte coalesced
+// loads into an LDS image [A][TT*4 (+4 pad)], and the output -- which for a fixed (b, p, c) and time chunk
+// is ONE contiguous run of TT*A u16 -- is written with 16-byte coalesced stores (8 antennas per lane).
+// The odd dword pitch (TT + 1) keeps the 2-byte transposed LDS reads bank-conflict-free.
+#include "bf_common.hpp"
+
+namespace bf {
+
+__global__ __launch_bounds__(256) void reorder_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                      int A, int C, int T, int TT, int nchunk) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_u32[];
+  const int chunk = blockIdx.x % nchunk;
+  const long long bc = blockIdx.x / nchunk;
+  const long long b = bc / C;
+  const int c = static_cast<int>(bc % C);
+  const int t0 = chunk * TT;
+  const int pitch = TT + 1;  // dwords per antenna row
+  const int quads = TT >> 2;
+
+  // 1. antenna runs -> LDS.  in[b][a][c][t][p][ri], one 16-byte load = 4 time samples x 2 pols x (re, im).
+  for (int idx = threadIdx.x; idx < A * quads; idx += blockDim.x) {
+    const int a = idx / quads;
+    const int tq = idx - a * quads;
+    const size_t src = ((static_cast<size_t>(b) * A + a) * C + c) * static_cast<size_t>(T) * 4 +
+                       static_cast<size_t>(t0 + 4 * tq) * 4;
+    const uint4 v = *reinterpret_cast<const uint4*>(in + src);
+    uint32_t* row = lds_u32 + a * pitch + 4 * tq;
+    row[0] = v.x;
+    row[1] = v.y;
+    row[2] = v.z;
+    row[3] = v.w;
+  }
+  __syncthreads();
+
+  // 2. LDS -> out[b][p][c][t][a][ri]: for each pol the chunk is TT*A contiguous u16 (16-byte aligned).
+  const uint16_t* lds_u16 = reinterpret_cast<const uint16_t*>(lds_u32);
+  const int n_u16 = TT * A;
+  for (int p = 0; p < 2; ++p) {
+    uint8_t* dst = out + ((static_cast<size_t>(b) * 2 + p) * C + c) * static_cast<size_t>(T) * A * 2 +
+                   static_cast<size_t>(t0) * A * 2;
+    for (int e0 = threadIdx.x * 8; e0 < n_u16; e0 += blockDim.x * 8) {
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t pair = 0;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int e = e0 + 2 * j + half;
+          const int t = e / A;
+          const int a = e - t * A;
+          // element (a, t, p) of the LDS image, in u16 units: a*pitch*2 + t*2 + p
+          pair |= static_cast<uint32_t>(lds_u16[a * pitch * 2 + t * 2 + p]) << (16 * half);
+        }
+        w[j] = pair;
+      }
+      *reinterpret_cast<uint4*>(dst + static_cast<size_t>(e0) * 2) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
+}  // namespace bf
+
+extern "C" int bf_reorder(const uint8_t* in, uint8_t* out, int B, int A, int C, int T, void* stream) {
+  BF_REQUIRE(in && out, "bf_reorder: null pointer");
+  BF_REQUIRE(B > 0 && A > 0 && C > 0 && T > 0, "bf_reorder: bad shape B=%d A=%d C=%d T=%d", B, A, C, T);
+  // the reference's check `T % (T // 16)` does not enforce this; the layout needs it.
+  BF_REQUIRE(T % bf::kSamplesPerBlock == 0, "bf_reorder: n_samples_per_channel=%d must be a multiple of 16", T);
+  BF_REQUIRE((reinterpret_cast<uintptr_t>(in) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
+             "bf_reorder: buffers must be 16-byte aligned");
+  // Largest power-of-two time chunk (>= 8, dividing T) whose LDS image fits 64 KiB.
+  int TT = 1;
+  while (TT * 2 <= T && T % (TT * 2) == 0) TT *= 2;
+  while (TT > 8 && static_cast<long long>(A) * (TT * 4 + 4) > 65536) TT /= 2;
+  BF_REQUIRE(static_cast<long long>(A) * (TT * 4 + 4) <= 65536, "bf_reorder: n_ants=%d too large", A);
+  const int nchunk = T / TT;
+  const long long grid = static_cast<long long>(B) * C * nchunk;
+  BF_REQUIRE(grid < (1LL << 31), "bf_reorder: grid too large");
+  const size_t lds = static_cast<size_t>(A) * (TT + 1) * 4;
+  hipLaunchKernelGGL(bf::reorder_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), lds, bf::as_stream(stream),
+                     in, out, A, C, T, TT, nchunk);
+  BF_LAUNCHED("reorder_kernel");
+}

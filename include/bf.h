@@ -1,0 +1,124 @@
+/*
+ * bf.h -- C ABI of libbf.so, the MI355X-native (gfx950) beamformer hot path.
+ *
+ * Drop-in boundary for the reference's operator package `beamformer/beamforming` (magnate3/dpdk_dc_sand).
+ * Every entry point below states the reference interface it replaces (file:line, relative to the reference
+ * repository root).  Conventions:
+ *   - every function returns int: 0 = OK, negative = error; bf_last_error() gives a thread-local message;
+ *   - compute entry points take caller-owned DEVICE pointers plus a stream (hipStream_t passed as void*,
+ *     NULL = the default stream), never allocate, are asynchronous and stream-ordered, and are reentrant
+ *     across streams;
+ *   - shapes are the reference's (B = batches, P = pols = 2, C = channels on this engine, Ctot = channels
+ *     in the band, A = antennas, M = beams, T = samples per channel, NB = T / 16);
+ *   - 8-bit voltages are complex (re, im) byte pairs; sample_signed = 0 reads them as uint8 (the reference
+ *     slots' dtype, matrix_multiply.py:145-147), 1 as int8 (the C++ study's char2, BeamformerKernels.cu:196).
+ */
+#ifndef DPDK_DC_SAND_AMD_BF_H
+#define DPDK_DC_SAND_AMD_BF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status ------------------------------------------------------------------------------------------- */
+#define BF_OK 0
+#define BF_ERR_ARG (-1)     /* invalid shape / argument (reference: template ValueError, prebeamform_reorder.py:62-65) */
+#define BF_ERR_HIP (-2)     /* HIP runtime error (reference: GPU_ERRCHK, common/Utils.hpp:8, common/Utils.cpp:8-16) */
+#define BF_ERR_NODEV (-3)   /* no GPU visible */
+
+/* Thread-local message of the last failing call on this thread (replaces GPU_ERRCHK's stderr print). */
+const char* bf_last_error(void);
+/* ABI version: major * 100 + minor. */
+int bf_abi_version(void);
+
+/* ---- runtime helpers (device memory, streams, events) -------------------------------------------------
+ * The reference gets these from katsdpsigproc.accel / PyCUDA (accel.create_some_context,
+ * ctx.create_command_queue, DeviceArray.set/get: beamform_op_sequence_test.py:105-163) and, in the C++
+ * harness, from the CUDA runtime (common/UnitTest.cpp:28-111).  Thin HIP wrappers so the Python shim needs
+ * no other GPU runtime. */
+int bf_device_count(int* count);
+int bf_set_device(int device);
+int bf_get_device(int* device);
+int bf_device_name(int device, char* buf, size_t len);
+int bf_malloc(void** ptr, size_t bytes);
+int bf_free(void* ptr);
+int bf_host_alloc(void** ptr, size_t bytes);   /* pinned host memory (streaming ring, cudaPcieRateTest.cpp:63-123) */
+int bf_host_free(void* ptr);
+int bf_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int bf_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int bf_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
+int bf_memset(void* dst, int value, size_t bytes, void* stream);
+int bf_stream_create(void** stream);
+int bf_stream_destroy(void* stream);
+int bf_stream_synchronize(void* stream);
+int bf_stream_wait_event(void* stream, void* event);
+int bf_device_synchronize(void);
+int bf_event_create(void** event);
+int bf_event_destroy(void* event);
+int bf_event_record(void* event, void* stream);
+int bf_event_synchronize(void* event);
+int bf_event_elapsed_ms(float* ms, void* start, void* stop);
+
+/* ---- hot path ----------------------------------------------------------------------------------------- */
+
+/* Steering coefficients, Python layout.
+ * Replaces CoeffGenerator._run -> run_coeff_gen (beamformer/beamforming/coeff_generator.py:12-103, 209-250),
+ * with the CPU oracle's (c, m, a) mapping (beamformer/unit_test/coeff_generator_cpu.py:120-186).
+ *   delay_vals : f32 (C, M, A, 4) = (delay_s, delay_rate, phase_rad, phase_rate); only [0] and [2] are read
+ *   out        : f32 (B, P, C, 2A, 2M), block [[cos, sin], [-sin, cos]] per (a, m), replicated over (b, p)
+ * The phase is evaluated in float64 in the reference's operation order, so the output is bit-exact to the
+ * oracle. */
+int bf_coeff_gen(const float* delay_vals, float* out, int B, int P, int C, int Ctot, int A, int M,
+                 int xeng_id, double sample_period, void* stream);
+
+/* Time-dependent compact coefficients (C++ study's steering kernels, BeamformerKernels.cu:7-189, with the
+ * Python sign convention):
+ *   rot(t, c, m, a) = (phi + phi_rate*dt) - pi*(tau + tau_rate*dt)*(ch - Ctot/2)/(Ctot*Ts),
+ *   dt = t0 + t*dt_step for t in [0, n_times)
+ *   delay_vals : f32 (Cd, M, A, 4) with Cd = C (per channel) or 1 (one model for every channel)
+ *   out        : (n_times, C, A, M) complex: out_fp16 = 0 -> float2 (re, im); 1 -> half2 (b16BitOutput,
+ *                BeamformerKernels.cu:111-116) */
+int bf_coeff_gen_time(const float* delay_vals, int delay_channels, void* out, int out_fp16, int n_times,
+                      int C, int Ctot, int A, int M, int xeng_id, double sample_period, double t0,
+                      double dt_step, void* stream);
+
+/* Pre-beamform reorder, bit-exact.
+ * Replaces PreBeamformReorder._run / prebeamform_reorder kernel (beamformer/beamforming/prebeamform_reorder.py:
+ * 171-186, kernels/prebeamform_reorder_kernel.mako:37-93):
+ *   in  : u8 (B, A, C, T, 2, 2)   out : u8 (B, 2, C, T/16, 16, A, 2).   T % 16 == 0. */
+int bf_reorder(const uint8_t* in, uint8_t* out, int B, int A, int C, int T, void* stream);
+
+/* Beamform complex multiply (MFMA batched GEMM, f16 hi/lo coefficient split, f32 accumulation).
+ * Replaces MatrixMultiply._run -> ComplexMultKernel.complex_mult -> run_complex_mult
+ * (beamformer/beamforming/matrix_multiply.py:155-163, complex_mult_kernel.py:11-100, 106-162):
+ *   x : 8-bit (B, P, C, NB, 16, A, 2)   w : f32 (B, P, C, 2A, 2M)   y : f32 (B, P, C, NB, 16, 2M)
+ *   y[..., col] = sum_k x[..., k] * w[k, col] with x[2a] = re, x[2a+1] = im. */
+int bf_beamform(const uint8_t* x, const float* w, float* y, int B, int P, int C, int NB, int A, int M,
+                int sample_signed, void* stream);
+
+/* Fused pre-beamform reorder + per-batch coefficient regeneration + beamform (one pass over the voltages).
+ * Replaces the OpSequence chain (beamformer/beamforming/beamform_op_sequence.py:117-157: reorder ->
+ * coeff gen -> multiply) and the C++ fused study kernel calculate_beamweights_and_beamform_single_channel
+ * (beamformer_coefficient_generator/BeamformerKernels.cu:192-367, correct complex multiply):
+ *   raw        : 8-bit (B, A, C, T, 2, 2), the reorder's input layout, read directly
+ *   delay_vals : f32 (Cd, M, A, 4), Cd = C or 1; batch b uses dt_b = t0 + b*batch_dt (regeneration per
+ *                block of T samples, BeamformerParameters.h:17); with zero rates/dt it equals OpSequence
+ *   y          : out_int8 = 0 -> f32 (B, 2, C, T/16, 16, 2M);
+ *                out_int8 = 1 -> int8 (B, 2, C, T/16, 16, 2M) = sat127(rne(y * out_scale)) (bf_requant). */
+int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, int delay_channels, void* y, int B, int C,
+                      int T, int A, int M, int Ctot, int xeng_id, double sample_period, double t0,
+                      double batch_dt, int sample_signed, int out_int8, float out_scale, void* stream);
+
+/* 8-bit requantiser (no reference counterpart; SURVEY §7 build step 7): q = clamp(rne(y*scale), -127, 127). */
+int bf_requant(const float* y, int8_t* q, size_t n, float scale, void* stream);
+
+/* Algorithmic HBM bytes of one bf_beamform_fused launch (bench / roofline bookkeeping). */
+double bf_fused_algorithmic_bytes(int B, int C, int T, int A, int M, int delay_channels, int out_int8);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPDK_DC_SAND_AMD_BF_H */

@@ -1,0 +1,145 @@
+"""NumPy restatement of the reference beamformer algorithms (TEST INFRASTRUCTURE ONLY; see __init__).
+
+Every function cites the reference file:line it restates.  Conventions:
+B = batches, P = pols (2), C = channels on this engine, Ctot = channels in the band, A = antennas,
+M = beams, T = samples per channel, NB = T // 16.
+"""
+import math
+
+import numpy as np
+
+TS_MEERKAT = 1 / 1712e6  # ADC sample period used by every reference test (e.g. beamform_op_sequence_test.py:90)
+SAMPLES_PER_BLOCK = 16  # matrix_multiply.py:76 (128 // 8)
+
+
+def u8_voltages(shape, seed=2021):
+    """The reference tests' voltage generator (beamform_op_sequence_test.py:143-149)."""
+    rng = np.random.default_rng(seed=seed)
+    return rng.uniform(np.iinfo(np.uint8).min, np.iinfo(np.uint8).max, shape).astype(np.uint8)
+
+
+def coeff_rotation(delay_vals, C, Ctot, xeng_id, Ts, dt=0.0):
+    """Steering phase in float64, in the reference's exact left-to-right operation order.
+
+    coeff_generator_cpu.py:125-164 (and coeff_generator.py:46-65):
+        initial = delay_s * ichannel * (-pi) / (Ctot * Ts) + phase_rad
+        centre  = delay_s * (Ctot / 2) * (-pi) / (Ctot * Ts)
+        rot     = initial - centre
+    Under numpy 1.x every step promotes to float64 (np.float32 * int -> float64).
+
+    Time extension (used by the fused per-block regeneration): the delay and phase are
+    first advanced by their rates, tau' = tau + tau_rate*dt and phi' = phi + phi_rate*dt, then the same
+    expression is evaluated; at dt == 0 this is bit-identical to the reference.
+    Returns float64 (C, M, A).
+    """
+    d = np.asarray(delay_vals, dtype=np.float32)
+    assert d.shape[0] == C and d.shape[-1] == 4
+    tau = d[..., 0].astype(np.float64)
+    phi = d[..., 2].astype(np.float64)
+    if dt != 0.0:
+        tau = tau + d[..., 1].astype(np.float64) * dt
+        phi = phi + d[..., 3].astype(np.float64) * dt
+    ch = (np.arange(C, dtype=np.int64) + C * xeng_id).astype(np.float64)[:, None, None]
+    denom = float(Ctot) * Ts
+    initial = tau * ch * (-math.pi) / denom + phi
+    centre = tau * (Ctot / 2) * (-math.pi) / denom
+    return initial - centre
+
+
+def _cos_sin_f32(rot):
+    # math.cos/sin (libm, as the reference's Python calls) then round to float32 on store.
+    flat = rot.ravel()
+    c = np.fromiter((math.cos(v) for v in flat), dtype=np.float64, count=flat.size)
+    s = np.fromiter((math.sin(v) for v in flat), dtype=np.float64, count=flat.size)
+    return c.astype(np.float32).reshape(rot.shape), s.astype(np.float32).reshape(rot.shape)
+
+
+def _pack_blocks(cos, sin, B, P):
+    """[[R, I], [-I, R]] 2x2 real blocks: W[2a][2m]=R, W[2a][2m+1]=I, W[2a+1][2m]=-I, W[2a+1][2m+1]=R
+    (coeff_generator_cpu.py:170-186), replicated over (batch, pol)."""
+    C, M, A = cos.shape
+    w = np.empty((C, A, 2, M, 2), np.float32)
+    cT = cos.transpose(0, 2, 1)
+    sT = sin.transpose(0, 2, 1)
+    w[:, :, 0, :, 0] = cT
+    w[:, :, 0, :, 1] = sT
+    w[:, :, 1, :, 0] = -sT
+    w[:, :, 1, :, 1] = cT
+    w = w.reshape(C, 2 * A, 2 * M)
+    return np.broadcast_to(w, (B, P, C, 2 * A, 2 * M)).copy()
+
+
+def coeffs(delay_vals, B, P, C, Ctot, A, M, xeng_id, Ts=TS_MEERKAT):
+    """CoeffGenerator.cpu_coeffs (coeff_generator_cpu.py:78-187): f32 (B, P, C, 2A, 2M).
+
+    delay_vals[c][m][a] feeds antenna a, beam m (the CPU oracle's mapping; the numba kernel's transposed
+    read, SURVEY A1, is not reproduced)."""
+    d = np.asarray(delay_vals, np.float32)
+    assert d.shape == (C, M, A, 4), d.shape
+    cos, sin = _cos_sin_f32(coeff_rotation(d, C, Ctot, xeng_id, Ts))
+    return _pack_blocks(cos, sin, B, P)
+
+
+def coeffs_at(delay_vals, C, Ctot, A, M, xeng_id, Ts, dt):
+    """Compact complex coefficients at time offset dt: (cos, sin) f32, each (C, M, A)."""
+    d = np.asarray(delay_vals, np.float32)
+    return _cos_sin_f32(coeff_rotation(d, C, Ctot, xeng_id, Ts, dt))
+
+
+def reorder(x):
+    """reorder.run_reorder (beamforming/reorder.py:40-42): (B,A,C,T,2,2) -> (B,2,C,T/16,16,A,2)."""
+    B, A, C, T, P, Z = x.shape
+    return np.ascontiguousarray(
+        x.reshape(B, A, C, T // SAMPLES_PER_BLOCK, SAMPLES_PER_BLOCK, P, Z).transpose(0, 5, 2, 3, 4, 1, 6))
+
+
+def _as_real(x, signed):
+    if signed:
+        return np.asarray(x).view(np.int8).astype(np.float32)
+    return np.asarray(x).astype(np.float32)
+
+
+def complex_mult(x, w, signed=False):
+    """complex_mult_cpu.complex_mult (unit_test/complex_mult_cpu.py:82-147), vectorised.
+
+    x: u8 (B,P,C,NB,16,A,2); w: f32 (B,P,C,2A,2M) -> f32 (B,P,C,NB,16,2M):
+        out[..., col] = sum_k X[..., k] * W[k, col],  X[2a] = re, X[2a+1] = im   (complex_mult_kernel.py:89-100)
+    Per-beam correct (the reference CPU loop reads beam-0 coefficients for every beam; the two agree
+    whenever coefficients are beam-uniform, which is what the reference tests use)."""
+    B, P, C, NB, S, A, Z = x.shape
+    X = _as_real(x, signed).reshape(B, P, C, NB * S, 2 * A)
+    Y = np.matmul(X, np.asarray(w, np.float32))
+    return Y.reshape(B, P, C, NB, S, -1)
+
+
+def op_sequence(raw, delay_vals, C, Ctot, A, M, xeng_id=0, Ts=TS_MEERKAT):
+    """OpSequence (beamform_op_sequence.py:117-157): reorder -> coeffs -> complex mult."""
+    B = raw.shape[0]
+    return complex_mult(reorder(raw), coeffs(delay_vals, B, 2, C, Ctot, A, M, xeng_id, Ts))
+
+
+def fused_beamform(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, signed=False):
+    """The fused MI355X operator's contract: reorder + per-batch coefficient regeneration + complex mult.
+
+    raw: (B, A, C, T, 2, 2) 8-bit; delay_vals: (C, M, A, 4) or compact (1, M, A, 4) (same model for every
+    channel).  Batch b uses coefficients at dt_b = t0 + b * batch_dt (the per-block regeneration of
+    BeamformerParameters.h:17 ACCUMULATIONS_BEFORE_NEW_COEFFS).  Output f32 (B, 2, C, T/16, 16, 2M)."""
+    B, A, C, T, P, Z = raw.shape
+    d = np.asarray(delay_vals, np.float32)
+    if d.shape[0] == 1 and C > 1:
+        d = np.broadcast_to(d, (C,) + d.shape[1:])
+    M = d.shape[1]
+    xr = reorder(raw)
+    out = np.empty((B, 2, C, T // 16, 16, 2 * M), np.float32)
+    for b in range(B):
+        cos, sin = coeffs_at(d, C, Ctot, A, M, xeng_id, Ts, t0 + b * batch_dt)
+        w = _pack_blocks(cos, sin, 1, 2)
+        out[b:b + 1] = complex_mult(xr[b:b + 1], w, signed=signed)
+    return out
+
+
+def requantise(y, scale):
+    """8-bit requantiser contract (the reference has none; SURVEY hard part 5): round-half-to-even of
+    y * scale, saturated to [-127, 127] (symmetric, so conjugation never overflows).  int8 output."""
+    v = np.rint(np.asarray(y, np.float32) * np.float32(scale))
+    return np.clip(v, -127, 127).astype(np.int8)

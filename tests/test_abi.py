@@ -1,0 +1,75 @@
+"""C-ABI checks that need no GPU: libbf.so loads, exports every symbol include/bf.h declares, the ctypes
+prototypes agree with the header, and argument validation fails before touching a device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from dpdk_dc_sand_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "bf.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*(?:const\s+)?[\w\s\*]+?\b(bf_\w+)\s*\(([^;]*?)\)\s*;", text, flags=re.M | re.S):
+        args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        out[m.group(1)] = len(args)
+    return out
+
+
+def test_header_parses():
+    decl = declared_functions()
+    assert {"bf_coeff_gen", "bf_reorder", "bf_beamform", "bf_beamform_fused", "bf_requant"} <= set(decl)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, f"libbf.so lacks {missing}"
+
+
+def test_prototypes_match_header():
+    decl = declared_functions()
+    assert set(decl) == set(_lib.PROTOTYPES), set(decl) ^ set(_lib.PROTOTYPES)
+    for name, nargs in decl.items():
+        assert len(_lib.PROTOTYPES[name][1]) == nargs, name
+
+
+def test_abi_version_and_error_channel():
+    lib = _lib.load()
+    assert lib.bf_abi_version() == 100
+    assert isinstance(_lib.last_error(), str)
+
+
+def test_argument_validation_without_gpu():
+    fake = 1 << 20  # 16-byte aligned, never dereferenced: validation fails first
+    with pytest.raises(_lib.BeamformerError, match="multiple of 16"):
+        _lib.call("bf_reorder", fake, fake, 1, 4, 4, 17, None)
+    with pytest.raises(_lib.BeamformerError, match="bad shape"):
+        _lib.call("bf_beamform", fake, fake, fake, 0, 2, 1, 1, 4, 1, 0, None)
+    with pytest.raises(_lib.BeamformerError, match="delay_channels"):
+        _lib.call("bf_beamform_fused", fake, fake, 3, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0, 0, 0, 1.0, None)
+    with pytest.raises(_lib.BeamformerError, match="null pointer"):
+        _lib.call("bf_coeff_gen", None, None, 1, 1, 1, 1, 1, 1, 0, 1e-9, None)
+    with pytest.raises(_lib.BeamformerError, match="misaligned"):
+        _lib.call("bf_beamform_fused", fake + 1, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0, 0, 0, 1.0,
+                  None)
+
+
+def test_algorithmic_bytes():
+    lib = _lib.load()
+    B, C, T, A, M = 8, 4096, 256, 64, 16
+    got = lib.bf_fused_algorithmic_bytes(B, C, T, A, M, 1, 0)
+    assert got == 2 * A * 2 * C * T * B + 8 * M * 2 * C * T * B + 16 * A * M
+    assert lib.bf_fused_algorithmic_bytes(B, C, T, A, M, 1, 1) == 2 * A * 2 * C * T * B + 2 * M * 2 * C * T * B + \
+        16 * A * M
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(OSError, match="no CPU fallback"):
+        _lib.load(str(tmp_path / "libbf.so"))

@@ -1,0 +1,297 @@
+"""GPU parity: the HIP operators (through the C ABI) against the goldens and the CPU oracle.
+
+Mirrors the reference's four GPU unit tests (beamformer/unit_test/*_test.py) -- same parameter grid
+(test_parameters.py), same input generators, same tolerances -- and adds what they mask:
+non-uniform per-(c, m, a) delays, xeng_id > 0, per-beam-varying coefficients, signed samples, odd shapes.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from dpdk_dc_sand_amd import _lib
+from dpdk_dc_sand_amd.beamforming import (CoeffGeneratorTemplate, FusedBeamformerTemplate, MatrixMultiplyTemplate,
+                                          OpSequenceTemplate, PreBeamformReorderTemplate, RequantTemplate)
+from golden_io import cases, get, voltages
+
+pytestmark = pytest.mark.gpu
+
+TS = O.TS_MEERKAT
+# beamformer/unit_test/test_parameters.py:5-36
+N_BATCHES = [3]
+N_ANTS = [4, 8, 16, 32, 64, 79, 80, 84, 130, 192, 256, 5, 23, 61, 19]
+N_SAMPLES = [256]
+N_CHANNELS = [1024, 4096, 32768]
+N_BEAMS = [2]
+XENG_ID = [0]
+SAMPLES_DELAY = [5]
+PHASE = [np.pi / 2]
+
+
+def uniform_delays(C, M, A, samples_delay=5, phase=np.pi / 2):
+    """beamform_coeff_test.py:86-112."""
+    d = np.zeros((C, M, A, 4), np.float32)
+    d[..., 0] = np.single(samples_delay * TS)
+    d[..., 2] = np.single(phase)
+    return d
+
+
+def random_delays(C, M, A, seed, rates=True):
+    rng = np.random.default_rng(seed)
+    d = np.zeros((C, M, A, 4), np.float32)
+    d[..., 0] = rng.uniform(0, 10 * TS, (C, M, A))
+    d[..., 2] = rng.uniform(-np.pi, np.pi, (C, M, A))
+    if rates:
+        d[..., 1] = rng.uniform(-1e-9, 1e-9, (C, M, A))
+        d[..., 3] = rng.uniform(-1.0, 1.0, (C, M, A))
+    return d
+
+
+def run(op, queue, inputs, outputs):
+    op.ensure_all_bound()
+    for name, host in inputs.items():
+        op.buffer(name).set(queue, host)
+    op()
+    return [op.buffer(name).get(queue) for name in outputs]
+
+
+def assert_beams_close(y, x_real, w):
+    """Error bound for the f16 hi/lo MFMA path against an exact (float64) product: each coefficient carries
+    <= 2^-22 relative (+ 2^-25 absolute) error and each f32 rounding of the running sum adds <= 2^-24 of it,
+    so |err| <= (3e-7 + 1.2e-7 * roundings) * sum_k |x_k w_k| + 1e-6.
+    x_real: (..., T, 2A) float; w: (..., 2A, 2M)."""
+    exact = np.matmul(x_real.astype(np.float64), w.astype(np.float64))
+    mag = np.matmul(np.abs(x_real).astype(np.float64), np.abs(w).astype(np.float64))
+    err = np.abs(y.reshape(exact.shape).astype(np.float64) - exact)
+    nsteps = 2 * ((w.shape[-2] + 31) // 32)  # f32 roundings of the running sum (hi and lo per k-step)
+    bound = (3e-7 + 1.2e-7 * nsteps) * mag + 1e-6
+    worst = float((err / bound).max()) if err.size else 0.0
+    assert worst <= 1.0, f"beam error exceeds the f32-class bound by {worst:.2f}x"
+
+
+# ---- pre-beamform reorder (prebeamform_reorder_test.py:33-122) -------------------------------------------
+@pytest.mark.parametrize("case", cases("reorder_"))
+def test_reorder_golden(context, command_queue, case):
+    B, A, C, T = (int(v) for v in get(case, "dims"))
+    x = voltages(case, (B, A, C, T, 2, 2))
+    op = PreBeamformReorderTemplate(context, A, C, T, B).instantiate(command_queue)
+    (y,) = run(op, command_queue, {"inSamples": x}, ["outReordered"])
+    np.testing.assert_array_equal(y, O.reorder(x))
+
+
+@pytest.mark.parametrize("n_batches", N_BATCHES)
+@pytest.mark.parametrize("n_ants", N_ANTS)
+@pytest.mark.parametrize("n_channels", N_CHANNELS)
+@pytest.mark.parametrize("n_samples_per_channel", N_SAMPLES)
+def test_prebeamform_reorder_parametrised(context, command_queue, n_batches, n_ants, n_channels,
+                                          n_samples_per_channel):
+    C = n_channels // n_ants // 4
+    op = PreBeamformReorderTemplate(context, n_ants=n_ants, n_channels_per_stream=C,
+                                    n_samples_per_channel=n_samples_per_channel,
+                                    n_batches=n_batches).instantiate(command_queue)
+    x = O.u8_voltages((n_batches, n_ants, C, n_samples_per_channel, 2, 2))
+    (y,) = run(op, command_queue, {"inSamples": x}, ["outReordered"])
+    np.testing.assert_array_equal(O.reorder(x), y)
+
+
+@pytest.mark.parametrize("A,C,T", [(1, 1, 16), (3, 7, 48), (257, 2, 64), (64, 3, 1024), (8, 1, 4096)])
+def test_reorder_edge_shapes(context, command_queue, A, C, T):
+    op = PreBeamformReorderTemplate(context, A, C, T, 2).instantiate(command_queue)
+    x = O.u8_voltages((2, A, C, T, 2, 2), seed=A * 1000 + T)
+    (y,) = run(op, command_queue, {"inSamples": x}, ["outReordered"])
+    np.testing.assert_array_equal(O.reorder(x), y)
+
+
+# ---- coefficient generator (beamform_coeff_test.py:29-172: bit-exact) ------------------------------------
+@pytest.mark.parametrize("case", cases("coeff_"))
+def test_coeffs_golden(context, command_queue, case):
+    B, P, C, Ctot, A, M, xeng_id = (int(v) for v in get(case, "dims"))
+    op = CoeffGeneratorTemplate(context, B, P, C, Ctot, 16, 16, A, M, xeng_id, TS).instantiate(command_queue)
+    (w,) = run(op, command_queue, {"delay_vals": get(case, "delays")}, ["outCoeffs"])
+    for b in range(B):
+        for p in range(P):
+            np.testing.assert_array_equal(w[b, p], get(case, "coeffs00"))
+
+
+@pytest.mark.parametrize("n_batches", N_BATCHES)
+@pytest.mark.parametrize("n_ants", N_ANTS)
+@pytest.mark.parametrize("n_channels", N_CHANNELS)
+@pytest.mark.parametrize("n_beams", N_BEAMS)
+@pytest.mark.parametrize("xeng_id", [0, 5])
+@pytest.mark.parametrize("kind", ["uniform", "random"])
+def test_beamform_coeffs(context, command_queue, n_batches, n_ants, n_channels, n_beams, xeng_id, kind):
+    C = n_channels // n_ants // 4
+    d = uniform_delays(C, n_beams, n_ants) if kind == "uniform" else random_delays(C, n_beams, n_ants, n_ants)
+    op = CoeffGeneratorTemplate(context, n_batches, 2, C, n_channels, 16, 16, n_ants, n_beams, xeng_id,
+                                TS).instantiate(command_queue)
+    (w,) = run(op, command_queue, {"delay_vals": d}, ["outCoeffs"])
+    np.testing.assert_array_equal(O.coeffs(d, n_batches, 2, C, n_channels, n_ants, n_beams, xeng_id), w)
+
+
+def test_coeff_gen_time_matches_oracle(context, command_queue):
+    from dpdk_dc_sand_amd import accel
+    C, A, M, Ctot, nt = 6, 5, 3, 4096, 4
+    d = random_delays(C, M, A, 7)
+    dv = accel.DeviceArray(context, d.shape, np.float32)
+    dv.set(command_queue, d)
+    out = accel.DeviceArray(context, (nt, C, A, M, 2), np.float32)
+    out16 = accel.DeviceArray(context, (nt, C, A, M, 2), np.float16)
+    t0, step = 1e-3, 8192 * TS
+    _lib.call("bf_coeff_gen_time", dv.ptr, C, out.ptr, 0, nt, C, Ctot, A, M, 2, TS, t0, step, command_queue.handle)
+    _lib.call("bf_coeff_gen_time", dv.ptr, C, out16.ptr, 1, nt, C, Ctot, A, M, 2, TS, t0, step, command_queue.handle)
+    got, got16 = out.get(command_queue), out16.get(command_queue)
+    for t in range(nt):
+        cos, sin = O.coeffs_at(d, C, Ctot, A, M, 2, TS, t0 + t * step)
+        np.testing.assert_array_equal(got[t, ..., 0], cos.transpose(0, 2, 1))
+        np.testing.assert_array_equal(got[t, ..., 1], sin.transpose(0, 2, 1))
+        np.testing.assert_array_equal(got16[t, ..., 0], cos.transpose(0, 2, 1).astype(np.float16))
+        np.testing.assert_array_equal(got16[t, ..., 1], sin.transpose(0, 2, 1).astype(np.float16))
+
+
+# ---- beamform multiply (beamform_mult_kernel_test.py:119-269: rtol = atol = 1e-4) -------------------------
+@pytest.mark.parametrize("case", cases("mult_"))
+def test_matrix_multiply_golden(context, command_queue, case):
+    B, A, M, Ctot, T, C = (int(v) for v in get(case, "dims"))
+    w = O.coeffs(get(case, "delays"), B, 2, C, Ctot, A, M, 0)
+    x = voltages(case, (B, 2, C, T // 16, 16, A, 2))
+    op = MatrixMultiplyTemplate(context, A, C, T, M, B).instantiate(command_queue)
+    (y,) = run(op, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
+    np.testing.assert_allclose(get(case, "output"), y, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.combinations(
+    "n_batches, n_ants, n_channels, n_samples_per_channel, n_beams, xeng_id, samples_delay, phase",
+    N_BATCHES, N_ANTS, N_CHANNELS, N_SAMPLES, N_BEAMS, XENG_ID, SAMPLES_DELAY, PHASE)
+def test_beamform(context, command_queue, n_batches, n_ants, n_channels, n_samples_per_channel, n_beams, xeng_id,
+                  samples_delay, phase):
+    """beamform_mult_kernel_test.py:119-269: coeff generator + multiply, reference tolerance."""
+    C = n_channels // n_ants // 4
+    d = uniform_delays(C, n_beams, n_ants, samples_delay, phase)
+    cg = CoeffGeneratorTemplate(context, n_batches, 2, C, n_channels, 16, 16, n_ants, n_beams, xeng_id,
+                                TS).instantiate(command_queue)
+    (w,) = run(cg, command_queue, {"delay_vals": d}, ["outCoeffs"])
+    x = O.u8_voltages((n_batches, 2, C, n_samples_per_channel // 16, 16, n_ants, 2))
+    mm = MatrixMultiplyTemplate(context, n_ants, C, n_samples_per_channel, n_beams, n_batches).instantiate(
+        command_queue)
+    (y,) = run(mm, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
+    ref = O.complex_mult(x, O.coeffs(d, n_batches, 2, C, n_channels, n_ants, n_beams, xeng_id))
+    np.testing.assert_allclose(ref, y, rtol=1e-04, atol=1e-04)
+
+
+@pytest.mark.parametrize("A,M,C,T,signed", [
+    (64, 16, 4, 256, False), (64, 16, 4, 256, True), (19, 3, 5, 64, False), (5, 1, 3, 32, True),
+    (130, 9, 2, 48, False), (256, 64, 1, 32, False), (61, 8, 3, 16, True), (2, 40, 2, 16, False)])
+def test_matrix_multiply_random_tables(context, command_queue, A, M, C, T, signed):
+    """Per-beam-varying coefficients (which the reference CPU oracle gets wrong) and int8 samples."""
+    B = 2
+    rng = np.random.default_rng(A * 7 + M)
+    x = rng.integers(0, 256, (B, 2, C, T // 16, 16, A, 2), dtype=np.uint8)
+    if signed:
+        x = x.view(np.int8)
+    d = random_delays(C, M, A, A + M)
+    w = O.coeffs(d, B, 2, C, 8192, A, M, 1)
+    w[1] *= rng.uniform(0.25, 2.0, w[1].shape).astype(np.float32)  # arbitrary table, not just phasors
+    op = MatrixMultiplyTemplate(context, A, C, T, M, B, sample_signed=signed).instantiate(command_queue)
+    (y,) = run(op, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
+    xr = (x.astype(np.float32) if not signed else x.astype(np.float32)).reshape(B, 2, C, T, 2 * A)
+    assert_beams_close(y, xr, w)
+    np.testing.assert_allclose(y, O.complex_mult(x, w, signed=signed), rtol=1e-4, atol=2e-3)
+
+
+# ---- full sequence (beamform_op_sequence_test.py:37-200) ---------------------------------------------------
+def test_op_sequence_golden(context, command_queue):
+    B, A, M, Ctot, T, C = (int(v) for v in get("opseq_cfg1", "dims"))
+    raw = voltages("opseq_cfg1", (B, A, C, T, 2, 2))
+    tmpl = OpSequenceTemplate(context, B, 2, C, Ctot, T // 16, 16, A, M, 0, TS, T)
+    op = tmpl.instantiate(command_queue)
+    op.ensure_all_bound()
+    op.beamform_coeff.buffer("delay_vals").set(command_queue, get("opseq_cfg1", "delays"))
+    op.prebeamform_reorder.buffer("inSamples").set(command_queue, raw)
+    op()
+    y = op.beamform_mult.buffer("outData").get(command_queue)
+    np.testing.assert_allclose(get("opseq_cfg1", "output"), y, rtol=1e-04, atol=1e-04)
+
+
+@pytest.mark.parametrize("n_batches", N_BATCHES)
+@pytest.mark.parametrize("n_ants", N_ANTS)
+@pytest.mark.parametrize("n_channels", N_CHANNELS)
+@pytest.mark.parametrize("n_beams", N_BEAMS)
+def test_beamform_op_sequence(context, command_queue, n_batches, n_ants, n_channels, n_beams):
+    C = n_channels // n_ants // 4
+    T = 256
+    d = uniform_delays(C, n_beams, n_ants)
+    op = OpSequenceTemplate(context, n_batches, 2, C, n_channels, T // 16, 16, n_ants, n_beams, 0, TS,
+                            T).instantiate(command_queue)
+    op.ensure_all_bound()
+    raw = O.u8_voltages((n_batches, n_ants, C, T, 2, 2))
+    op.beamform_coeff.buffer("delay_vals").set(command_queue, d)
+    op.prebeamform_reorder.buffer("inSamples").set(command_queue, raw)
+    op()
+    y = op.beamform_mult.buffer("outData").get(command_queue)
+    np.testing.assert_allclose(O.op_sequence(raw, d, C, n_channels, n_ants, n_beams), y, rtol=1e-04, atol=1e-04)
+
+
+# ---- fused one-pass operator --------------------------------------------------------------------------------
+def test_fused_equals_op_sequence_bitwise(context, command_queue):
+    """Same coefficients (float64 phase), same fragment order, same accumulation: identical bits."""
+    B, A, M, C, Ctot, T = 2, 64, 16, 8, 4096, 256
+    d = random_delays(C, M, A, 11, rates=False)
+    raw = O.u8_voltages((B, A, C, T, 2, 2), seed=3)
+    seq = OpSequenceTemplate(context, B, 2, C, Ctot, T // 16, 16, A, M, 2, TS, T).instantiate(command_queue)
+    seq.ensure_all_bound()
+    seq.beamform_coeff.buffer("delay_vals").set(command_queue, d)
+    seq.prebeamform_reorder.buffer("inSamples").set(command_queue, raw)
+    seq()
+    y_seq = seq.beamform_mult.buffer("outData").get(command_queue)
+    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=2, sample_period=TS).instantiate(command_queue)
+    (y_fu,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    np.testing.assert_array_equal(y_fu, y_seq)
+    np.testing.assert_allclose(y_fu, O.op_sequence(raw, d, C, Ctot, A, M, xeng_id=2), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
+    (64, 16, 4, 256, 3, 1, True), (64, 1, 4, 256, 2, 4, False), (4, 1, 64, 1024, 1, 64, False),
+    (19, 2, 13, 256, 3, 1, False), (5, 3, 7, 48, 2, 7, True), (130, 9, 2, 64, 2, 1, False),
+    (256, 64, 1, 32, 1, 1, True), (80, 2, 3, 16, 3, 3, False)])
+def test_fused_matches_oracle(context, command_queue, A, M, C, T, B, dch, signed):
+    Ctot, xeng = 8192, 3
+    d = random_delays(dch, M, A, A * 31 + M)
+    rng = np.random.default_rng(A + M + C)
+    raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8)
+    if signed:
+        raw = raw.view(np.int8)
+    t0, bdt = 2.5e-3, 256 * 8192 * TS
+    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, sample_period=TS, delay_channels=dch,
+                                 sample_signed=signed, t0=t0, batch_dt=bdt).instantiate(command_queue)
+    (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    ref = O.fused_beamform(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, signed=signed)
+    np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_fused_int8_output_is_requantised_f32(context, command_queue):
+    B, A, M, C, T, Ctot = 2, 64, 16, 4, 256, 4096
+    d = random_delays(1, M, A, 9)
+    raw = O.u8_voltages((B, A, C, T, 2, 2), seed=9).view(np.int8)
+    scale = 1.0 / 64
+    f32 = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, delay_channels=1, sample_signed=True).instantiate(
+        command_queue)
+    (y,) = run(f32, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    i8 = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, delay_channels=1, sample_signed=True, out_int8=True,
+                                 out_scale=scale).instantiate(command_queue)
+    (q,) = run(i8, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    np.testing.assert_array_equal(q, O.requantise(y, scale))
+    rq = RequantTemplate(context, y.shape, scale).instantiate(command_queue)
+    (q2,) = run(rq, command_queue, {"inData": y}, ["outData"])
+    np.testing.assert_array_equal(q2, q)
+
+
+# ---- errors --------------------------------------------------------------------------------------------------
+def test_errors_raise(context, command_queue):
+    with pytest.raises(ValueError):
+        PreBeamformReorderTemplate(context, 4, 4, 100, 1)
+    from dpdk_dc_sand_amd import accel
+    a = accel.DeviceArray(context, (64,), np.uint8)
+    with pytest.raises(_lib.BeamformerError, match="multiple of 16"):
+        _lib.call("bf_reorder", a.ptr, a.ptr, 1, 1, 1, 17, command_queue.handle)
+    op = MatrixMultiplyTemplate(context, 4, 2, 32, 1, 1).instantiate(command_queue)
+    with pytest.raises(ValueError):
+        op.bind(inData=accel.DeviceArray(context, (3,), np.uint8))

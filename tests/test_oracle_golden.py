@@ -1,0 +1,68 @@
+"""The CPU oracle (oracle/) against golden vectors produced by the reference's own CPU oracles.
+
+Pins: coefficients bit-exact (coeff_generator_cpu.py:78-187), reorder bit-exact (reorder.py:40-42), multiply and
+the full OpSequence chain within the reference tests' rtol = atol = 1e-4 (beamform_mult_kernel_test.py:267-269,
+beamform_op_sequence_test.py:198-200).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_io import cases, get, sha256, voltages
+
+
+@pytest.mark.parametrize("case", cases("reorder_"))
+def test_reorder_golden(case):
+    B, A, C, T = (int(v) for v in get(case, "dims"))
+    x = voltages(case, (B, A, C, T, 2, 2))
+    y = O.reorder(x)
+    assert y.shape == tuple(get(case, "output_shape"))
+    assert sha256(y) == str(get(case, "output_sha256"))
+
+
+@pytest.mark.parametrize("case", cases("coeff_"))
+def test_coeffs_golden(case):
+    B, P, C, Ctot, A, M, xeng_id = (int(v) for v in get(case, "dims"))
+    w = O.coeffs(get(case, "delays"), B, P, C, Ctot, A, M, xeng_id)
+    np.testing.assert_array_equal(w[0, 0], get(case, "coeffs00"))
+    assert sha256(w) == str(get(case, "coeffs_sha256"))
+
+
+@pytest.mark.parametrize("case", cases("mult_"))
+def test_complex_mult_golden(case):
+    B, A, M, Ctot, T, C = (int(v) for v in get(case, "dims"))
+    w = O.coeffs(get(case, "delays"), B, 2, C, Ctot, A, M, 0)
+    assert sha256(w) == str(get(case, "coeffs_sha256"))
+    x = voltages(case, (B, 2, C, T // 16, 16, A, 2))
+    np.testing.assert_allclose(O.complex_mult(x, w), get(case, "output"), rtol=1e-4, atol=1e-4)
+
+
+def test_op_sequence_golden():
+    B, A, M, Ctot, T, C = (int(v) for v in get("opseq_cfg1", "dims"))
+    raw = voltages("opseq_cfg1", (B, A, C, T, 2, 2))
+    y = O.op_sequence(raw, get("opseq_cfg1", "delays"), C, Ctot, A, M)
+    np.testing.assert_allclose(y, get("opseq_cfg1", "output"), rtol=1e-4, atol=1e-4)
+
+
+def test_fused_contract_reduces_to_op_sequence():
+    """With zero rates/dt the fused contract equals reorder -> coeffs -> multiply exactly."""
+    B, A, M, Ctot, T, C = (int(v) for v in get("opseq_cfg1", "dims"))
+    raw = voltages("opseq_cfg1", (B, A, C, T, 2, 2))
+    d = get("opseq_cfg1", "delays")
+    np.testing.assert_array_equal(O.fused_beamform(raw, d, Ctot), O.op_sequence(raw, d, C, Ctot, A, M))
+
+
+def test_time_extension_at_zero_is_reference_phase():
+    rng = np.random.default_rng(5)
+    d = rng.uniform(-1, 1, (3, 2, 5, 4)).astype(np.float32)
+    d[..., 0] *= 1e-8
+    r0 = O.coeff_rotation(d, 3, 1024, 2, O.TS_MEERKAT)
+    r1 = O.coeff_rotation(d, 3, 1024, 2, O.TS_MEERKAT, dt=0.0)
+    np.testing.assert_array_equal(r0, r1)
+    r2 = O.coeff_rotation(d, 3, 1024, 2, O.TS_MEERKAT, dt=1e-3)
+    assert not np.array_equal(r0, r2)
+
+
+def test_requantise_contract():
+    y = np.array([0.5, 1.5, 2.5, -0.5, -1.5, 126.6, 1e9, -1e9, np.float32(127.49)], np.float32)
+    np.testing.assert_array_equal(O.requantise(y, 1.0), [0, 2, 2, 0, -2, 127, 127, -127, 127])
