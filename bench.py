@@ -1,0 +1,268 @@
+"""Headline benchmark: int8 voltage Gsamples/s through the fused MI355X beamformer (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg2] [--no-cpu-baseline] [--no-pmc]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+
+A "step" is one pass of the hot path over one batch block of synthetic input already resident in HBM: one
+`bf_beamform_fused` launch = pre-beamform reorder (fused) + per-batch steering-coefficient regeneration from the
+delay model + the antenna x beam complex contraction, for every (batch, pol, channel, sample) of the shard.
+Workload cfg3 (default, BASELINE configs[2], the north-star target): 64 antennas, 16 beams, 4096 channels per
+GPU, T = 256 samples, B = 8 batches, dual-pol int8 voltages, float32 beams.  cfg2 (configs[1]): 1 beam.
+Frequency channels shard across ranks with no data-path collective (rank r = X-engine r, channels
+[4096 r, 4096 (r+1)) of a 4096*N-channel band): scaling is weak.
+
+Rank 0 prints ONE JSON line.  `value` = samples all ranks processed / max-over-ranks wall time of the K timed
+steps (barrier + device sync on both sides).  `roofline.achieved` = algorithmic bytes per launch / average
+launch duration from HIP events on the launch stream.  `roofline.traffic` = HBM bytes per launch from
+rocprofv3 PMC counters (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate passes), rank 0, N = 1.
+`cpu_baseline` = the oracle's vectorised NumPy restatement on a bounded channel sample, rank 0, N = 1.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "int8 voltage Gsamples/s ingested + beams/s, 64-ant 4096-ch; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6290 measured float4 copy
+TS = 1 / 1712e6
+
+WORKLOADS = {
+    "cfg3": dict(A=64, M=16, C=4096, T=256, B=8, desc="64 ants, 16 beams, 4096 ch/GPU, T=256, B=8, dual-pol int8, "
+                 "per-batch coefficient regeneration fused (BASELINE configs[2])"),
+    "cfg2": dict(A=64, M=1, C=4096, T=256, B=8, desc="64 ants, 1 beam, 4096 ch/GPU, T=256, B=8, dual-pol int8 "
+                 "(BASELINE configs[1])"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
+    p.add_argument("--out-int8", action="store_true", help="int8 requantised beams instead of float32")
+    p.add_argument("--nbuf", type=int, default=2, help="rotating input/output buffer sets (defeat the 256 MB MALL)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-pmc", action="store_true")
+    p.add_argument("--no-secondary", action="store_true")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return p.parse_args()
+
+
+class Dist:
+    """Barrier + max-reduction across ranks (gloo, CPU): the timing bracket only; no data-path collective."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist  # imported before libbf so one HIP runtime serves both
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, v):
+        if not self.dist:
+            return v
+        import torch
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def make_inputs(np, rng, shape, nbuf):
+    return [rng.integers(-128, 128, size=shape, dtype=np.int8) for _ in range(nbuf)]
+
+
+def run_gpu(args, dist, wl):
+    import numpy as np
+
+    from dpdk_dc_sand_amd import _lib, accel
+    from dpdk_dc_sand_amd.beamforming import FusedBeamformerTemplate
+
+    n_dev = accel.device_count()
+    if n_dev < 1:
+        raise RuntimeError("no HIP device visible")
+    ctx = accel.create_some_context(device=dist.local_rank % n_dev)
+    queue = ctx.create_command_queue()
+    A, M, C, T, B = wl["A"], wl["M"], wl["C"], wl["T"], wl["B"]
+    Ctot = C * max(dist.world, 1)
+    tmpl = FusedBeamformerTemplate(ctx, B, C, Ctot, T, A, M, xeng_id=dist.rank, sample_period=TS, delay_channels=1,
+                                   sample_signed=True, out_int8=args.out_int8, out_scale=1 / 64,
+                                   t0=0.0, batch_dt=T * 2 * Ctot * TS)
+    rng = np.random.default_rng(1 + dist.rank)
+    d = np.zeros(tmpl.delay_shape, np.float32)  # compact (1, M, A, 4) polynomial delay model with rates
+    d[..., 0] = rng.uniform(0, 10 * TS, d.shape[:-1])
+    d[..., 1] = rng.uniform(-1e-9, 1e-9, d.shape[:-1])
+    d[..., 2] = rng.uniform(-np.pi, np.pi, d.shape[:-1])
+    d[..., 3] = rng.uniform(-1, 1, d.shape[:-1])
+    ops = []
+    for i, host in enumerate(make_inputs(np, rng, tmpl.input_shape, args.nbuf)):
+        op = tmpl.instantiate(queue)
+        op.ensure_all_bound()
+        op.buffer("inSamples").set(queue, host)
+        op.buffer("delay_vals").set(queue, d)
+        ops.append(op)
+    del host
+    for i in range(args.warmup):
+        ops[i % len(ops)]()
+    queue.finish()
+
+    e0, e1 = accel.Event(), accel.Event()
+    dist.barrier()
+    queue.finish()
+    t0 = time.perf_counter()
+    e0.record(queue)
+    for i in range(args.steps):
+        ops[i % len(ops)]()
+    e1.record(queue)
+    queue.finish()
+    t_local = time.perf_counter() - t0
+    dist.barrier()
+    kernel_s = e1.time_since(e0) / args.steps
+    t_max = dist.max(t_local)
+    samples_per_step = A * 2 * C * T * B  # complex 8-bit samples (ant, pol, chan, time, batch)
+    beams_per_step = M * 2 * C * T * B
+    return dict(t_max=t_max, kernel_s=kernel_s, samples_per_step=samples_per_step, beams_per_step=beams_per_step,
+                alg_bytes=tmpl.algorithmic_bytes(), device=ctx.device.name,
+                out=(ops, queue))
+
+
+def cpu_baseline(wl, seconds=10.0):
+    """The oracle's vectorised NumPy restatement (reorder -> per-batch coefficients -> f32 matmul) timed on
+    this host on a bounded channel sample of the same workload (kind "port")."""
+    import numpy as np
+
+    import oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    A, M, T, B = wl["A"], wl["M"], wl["T"], wl["B"]
+    rng = np.random.default_rng(7)
+    d = np.zeros((1, M, A, 4), np.float32)
+    d[..., 0] = rng.uniform(0, 10 * TS, d.shape[:-1])
+    d[..., 2] = rng.uniform(-np.pi, np.pi, d.shape[:-1])
+
+    def once(c):
+        raw = rng.integers(-128, 128, size=(B, A, c, T, 2, 2), dtype=np.int8)
+        t = time.perf_counter()
+        O.fused_beamform(raw, d, wl["C"], signed=True, batch_dt=T * 2 * wl["C"] * TS)
+        return time.perf_counter() - t
+
+    c = 16
+    dt = once(c)  # warm-up + rate estimate
+    c = int(min(max(16, c * seconds / max(dt, 1e-3)), wl["C"]))
+    dt = once(c)
+    rate = A * 2 * c * T * B / dt / 1e9
+    return {"value": round(rate, 4), "unit": "Gsamples/s", "cores": int(threads), "kind": "port",
+            "sample": f"{c} of {wl['C']} channels x B={B} x T={T} x A={A} x 2 pols ({dt:.1f} s): oracle.fused_beamform "
+                      f"(NumPy reorder + float64-phase coefficients + float32 matmul, BLAS threads={threads})"}
+
+
+def pmc_traffic(args):
+    """HBM bytes per fused launch from rocprofv3 counters: FETCH_SIZE and WRITE_SIZE in separate passes
+    (MI355X_MICROARCH.md: gfx950 FETCH_SIZE reads 1/2 of a wide coalesced stream -> x2; WRITE_SIZE exact; KiB)."""
+    exe = "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, "rocprofv3 not found"
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = tempfile.mkdtemp(prefix="bfpmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
+               "--steps", "3", "--warmup", "1"] + (["--out-int8"] if args.out_int8 else [])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            return None, f"rocprofv3 {counter} failed rc={r.returncode}: {r.stderr[-300:]}"
+        per = []
+        with open(files[0]) as f:
+            for row in csv.DictReader(f):
+                if "beamform_fused" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    per.append(float(row["Counter_Value"]))
+        if not per:
+            return None, f"no {counter} rows for the fused kernel"
+        vals[counter] = sorted(per)[len(per) // 2]
+    traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+    return traffic, vals
+
+
+def main():
+    args = parse()
+    wl = WORKLOADS[args.workload]
+    dist = Dist()
+    if args.pmc_child:
+        run_gpu(args, dist, wl)
+        return
+    r = run_gpu(args, dist, wl)
+    ops_queue = r.pop("out")
+    total_samples = r["samples_per_step"] * args.steps * dist.world
+    value = total_samples / r["t_max"] / 1e9
+    achieved = r["alg_bytes"] / r["kernel_s"] / 1e9
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "Gsamples/s", "n_gpus": dist.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["t_max"] / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "data": "synthetic (uniform random int8 voltages, random delay/phase polynomials)",
+        "config": {"workload": args.workload + ": " + wl["desc"], "n_ants": wl["A"], "n_beams": wl["M"],
+                   "n_channels_per_gpu": wl["C"], "n_samples_per_channel": wl["T"], "n_batches": wl["B"],
+                   "n_pols": 2, "output": "int8" if args.out_int8 else "float32",
+                   "parallelism": f"channel-shard x{dist.world} (xeng_id = rank), no data-path collective"},
+        "beams_per_s": round(r["beams_per_step"] * args.steps * dist.world / r["t_max"], 1),
+        "compute": "f16 hi/lo-split coefficients on v_mfma_f32_16x16x32_f16, f32 accumulation",
+        "device": r["device"],
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "beamform_fused_kernel", "avg_launch_us": round(r["kernel_s"] * 1e6, 2),
+                     "alg_bytes_per_launch": r["alg_bytes"]},
+        "cpu_baseline": None,
+    }
+    del ops_queue
+    if dist.rank == 0 and dist.world == 1 and not args.no_secondary and args.workload == "cfg3":
+        try:
+            sub = argparse.Namespace(**{**vars(args), "workload": "cfg2"})
+            r2 = run_gpu(sub, dist, WORKLOADS["cfg2"])
+            r2.pop("out")
+            line["secondary"] = {
+                "workload": "cfg2: " + WORKLOADS["cfg2"]["desc"],
+                "value": round(r2["samples_per_step"] * args.steps / r2["t_max"] / 1e9, 2), "unit": "Gsamples/s",
+                "roofline_frac": round(r2["alg_bytes"] / r2["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
+                "avg_launch_us": round(r2["kernel_s"] * 1e6, 2)}
+        except Exception as e:  # secondary line is informational
+            line["secondary"] = {"error": str(e)[:200]}
+    if dist.rank == 0 and dist.world == 1 and not args.no_pmc:
+        try:
+            traffic, info = pmc_traffic(args)
+            line["roofline"]["traffic"] = traffic
+            line["roofline"]["traffic_counters"] = info
+        except Exception as e:
+            line["roofline"]["traffic_counters"] = f"unavailable: {str(e)[:200]}"
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(wl)
+    if dist.rank == 0:
+        print(json.dumps(line), flush=True)
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

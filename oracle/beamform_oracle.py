@@ -125,17 +125,28 @@ def fused_beamform(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batc
     channel).  Batch b uses coefficients at dt_b = t0 + b * batch_dt (the per-block regeneration of
     BeamformerParameters.h:17 ACCUMULATIONS_BEFORE_NEW_COEFFS).  Output f32 (B, 2, C, T/16, 16, 2M)."""
     B, A, C, T, P, Z = raw.shape
+    w = fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt)
+    return complex_mult(reorder(raw), w, signed=signed)
+
+
+def fused_tables(delay_vals, B, C, Ctot, A, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0):
+    """The (B, 2, C, 2A, 2M) coefficient tables the fused operator applies (batch b at dt = t0 + b*batch_dt)."""
     d = np.asarray(delay_vals, np.float32)
     if d.shape[0] == 1 and C > 1:
         d = np.broadcast_to(d, (C,) + d.shape[1:])
     M = d.shape[1]
-    xr = reorder(raw)
-    out = np.empty((B, 2, C, T // 16, 16, 2 * M), np.float32)
+    w = np.empty((B, 2, C, 2 * A, 2 * M), np.float32)
     for b in range(B):
         cos, sin = coeffs_at(d, C, Ctot, A, M, xeng_id, Ts, t0 + b * batch_dt)
-        w = _pack_blocks(cos, sin, 1, 2)
-        out[b:b + 1] = complex_mult(xr[b:b + 1], w, signed=signed)
-    return out
+        w[b] = _pack_blocks(cos, sin, 1, 2)[0]
+    return w
+
+
+def dot_magnitude(x, w, signed=False):
+    """sum_k |x_k| |w_k| per output (float64): the scale of fp32 rounding in each beam's dot product."""
+    B, P, C, NB, S, A, Z = x.shape
+    X = np.abs(_as_real(x, signed).reshape(B, P, C, NB * S, 2 * A)).astype(np.float64)
+    return np.matmul(X, np.abs(np.asarray(w, np.float64))).reshape(B, P, C, NB, S, -1)
 
 
 def requantise(y, scale):

@@ -12,6 +12,7 @@ from dpdk_dc_sand_amd import _lib
 from dpdk_dc_sand_amd.beamforming import (CoeffGeneratorTemplate, FusedBeamformerTemplate, MatrixMultiplyTemplate,
                                           OpSequenceTemplate, PreBeamformReorderTemplate, RequantTemplate)
 from golden_io import cases, get, voltages
+from tolerance import assert_beams_allclose
 
 pytestmark = pytest.mark.gpu
 
@@ -155,7 +156,7 @@ def test_matrix_multiply_golden(context, command_queue, case):
     x = voltages(case, (B, 2, C, T // 16, 16, A, 2))
     op = MatrixMultiplyTemplate(context, A, C, T, M, B).instantiate(command_queue)
     (y,) = run(op, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
-    np.testing.assert_allclose(get(case, "output"), y, rtol=1e-4, atol=1e-4)
+    assert_beams_allclose(y, get(case, "output"), x, w)
 
 
 @pytest.mark.combinations(
@@ -173,8 +174,8 @@ def test_beamform(context, command_queue, n_batches, n_ants, n_channels, n_sampl
     mm = MatrixMultiplyTemplate(context, n_ants, C, n_samples_per_channel, n_beams, n_batches).instantiate(
         command_queue)
     (y,) = run(mm, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
-    ref = O.complex_mult(x, O.coeffs(d, n_batches, 2, C, n_channels, n_ants, n_beams, xeng_id))
-    np.testing.assert_allclose(ref, y, rtol=1e-04, atol=1e-04)
+    w_ref = O.coeffs(d, n_batches, 2, C, n_channels, n_ants, n_beams, xeng_id)
+    assert_beams_allclose(y, O.complex_mult(x, w_ref), x, w_ref)
 
 
 @pytest.mark.parametrize("A,M,C,T,signed", [
@@ -192,9 +193,8 @@ def test_matrix_multiply_random_tables(context, command_queue, A, M, C, T, signe
     w[1] *= rng.uniform(0.25, 2.0, w[1].shape).astype(np.float32)  # arbitrary table, not just phasors
     op = MatrixMultiplyTemplate(context, A, C, T, M, B, sample_signed=signed).instantiate(command_queue)
     (y,) = run(op, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
-    xr = (x.astype(np.float32) if not signed else x.astype(np.float32)).reshape(B, 2, C, T, 2 * A)
-    assert_beams_close(y, xr, w)
-    np.testing.assert_allclose(y, O.complex_mult(x, w, signed=signed), rtol=1e-4, atol=2e-3)
+    assert_beams_close(y, x.astype(np.float32).reshape(B, 2, C, T, 2 * A), w)
+    assert_beams_allclose(y, O.complex_mult(x, w, signed=signed), x, w, signed=signed)
 
 
 # ---- full sequence (beamform_op_sequence_test.py:37-200) ---------------------------------------------------
@@ -208,7 +208,8 @@ def test_op_sequence_golden(context, command_queue):
     op.prebeamform_reorder.buffer("inSamples").set(command_queue, raw)
     op()
     y = op.beamform_mult.buffer("outData").get(command_queue)
-    np.testing.assert_allclose(get("opseq_cfg1", "output"), y, rtol=1e-04, atol=1e-04)
+    d = get("opseq_cfg1", "delays")
+    assert_beams_allclose(y, get("opseq_cfg1", "output"), O.reorder(raw), O.coeffs(d, B, 2, C, Ctot, A, M, 0))
 
 
 @pytest.mark.parametrize("n_batches", N_BATCHES)
@@ -227,7 +228,8 @@ def test_beamform_op_sequence(context, command_queue, n_batches, n_ants, n_chann
     op.prebeamform_reorder.buffer("inSamples").set(command_queue, raw)
     op()
     y = op.beamform_mult.buffer("outData").get(command_queue)
-    np.testing.assert_allclose(O.op_sequence(raw, d, C, n_channels, n_ants, n_beams), y, rtol=1e-04, atol=1e-04)
+    w = O.coeffs(d, n_batches, 2, C, n_channels, n_ants, n_beams, 0)
+    assert_beams_allclose(y, O.op_sequence(raw, d, C, n_channels, n_ants, n_beams), O.reorder(raw), w)
 
 
 # ---- fused one-pass operator --------------------------------------------------------------------------------
@@ -245,7 +247,8 @@ def test_fused_equals_op_sequence_bitwise(context, command_queue):
     fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=2, sample_period=TS).instantiate(command_queue)
     (y_fu,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     np.testing.assert_array_equal(y_fu, y_seq)
-    np.testing.assert_allclose(y_fu, O.op_sequence(raw, d, C, Ctot, A, M, xeng_id=2), rtol=1e-4, atol=1e-4)
+    assert_beams_allclose(y_fu, O.op_sequence(raw, d, C, Ctot, A, M, xeng_id=2), O.reorder(raw),
+                          O.coeffs(d, B, 2, C, Ctot, A, M, 2))
 
 
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
@@ -264,7 +267,8 @@ def test_fused_matches_oracle(context, command_queue, A, M, C, T, B, dch, signed
                                  sample_signed=signed, t0=t0, batch_dt=bdt).instantiate(command_queue)
     (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     ref = O.fused_beamform(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, signed=signed)
-    np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
+    w = O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, t0=t0, batch_dt=bdt)
+    assert_beams_allclose(y, ref, O.reorder(raw), w, signed=signed)
 
 
 def test_fused_int8_output_is_requantised_f32(context, command_queue):
