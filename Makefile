@@ -6,11 +6,11 @@ CSRC     := dpdk_dc_sand_amd/csrc
 LIB      := dpdk_dc_sand_amd/libbf.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -munsafe-fp-atomics
 SRCS     := $(CSRC)/bf_runtime.cpp $(CSRC)/bf_coeff.hip $(CSRC)/bf_reorder.hip $(CSRC)/bf_beamform.hip \
-            $(CSRC)/bf_requant.hip
+            $(CSRC)/bf_fused.hip $(CSRC)/bf_requant.hip
 OBJS     := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 HDRS     := $(wildcard $(CSRC)/*.hpp) include/bf.h
 
-.PHONY: all clean
+.PHONY: all clean diag
 all: $(LIB)
 
 build/%.o: $(CSRC)/% $(HDRS)
@@ -22,3 +22,10 @@ $(LIB): $(OBJS)
 
 clean:
 	rm -rf build $(LIB)
+
+# Diagnostic build (ablation variants + HBM stream kernel); used only by tools/diag_*.py, never by the product.
+DIAG_LIB := build/libbf_diag.so
+diag: $(DIAG_LIB)
+$(DIAG_LIB): $(SRCS) $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -DBF_DIAG -shared -o $@ $(SRCS)

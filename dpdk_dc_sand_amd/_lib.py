@@ -50,10 +50,14 @@ PROTOTYPES = {
     "bf_beamform": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_void_p]),
     "bf_beamform_fused": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-                                  c_int, c_double, c_double, c_double, c_int, c_int, c_float, c_void_p]),
+                                  c_int, c_double, c_double, c_double, c_int, c_float, c_void_p]),
     "bf_requant": (c_int, [c_void_p, c_void_p, c_size_t, c_float, c_void_p]),
     "bf_fused_algorithmic_bytes": (c_double, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
 }
+
+
+# bf_beamform_fused flags (include/bf.h)
+FUSED_SIGNED, FUSED_OUT_INT8, FUSED_EXACT_COEFF = 1, 2, 4
 
 
 class BeamformerError(RuntimeError):

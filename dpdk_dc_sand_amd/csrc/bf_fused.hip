@@ -1,0 +1,500 @@
+// Fused pre-beamform reorder + per-batch coefficient regeneration + beamform (one pass over the voltages).
+//
+// Replaces the reference's three-pass OpSequence (beamform_op_sequence.py:117-157: the reorder reads and writes
+// the whole cube, prebeamform_reorder_kernel.mako:37-93; the coefficient generator writes a (B, P, C, 2A, 2M)
+// f32 table replicated over batches and pols; the multiply reads both back) and the C++ study's fused kernel
+// calculate_beamweights_and_beamform_single_channel (BeamformerKernels.cu:192-367: one sincos per MAC, a shuffle
+// tree per sample, a non-complex product).
+//
+// Voltages are read straight from the raw (B, A, C, T, 2, 2) layout: each antenna's (t, p, re/im) run is
+// contiguous, so one 16-byte load is 4 samples x 2 pols of one antenna, and the loaded dwords feed the MFMA
+// B-operand fragments directly through v_perm (bf_mfma.hpp) -- the reorder costs no HBM traffic.  Coefficients
+// for each (b, c) are generated in-kernel from the delay model into LDS (hi/lo f16 fragments):
+//   exact mode: float64 phase in the reference's operation order + float64 sincos, bit-exact to CoeffGenerator
+//               (with zero rates the fused output equals OpSequence's bit for bit);
+//   fast mode (default): float64 argument without divisions, reduced mod 2 pi, float32 sincos with a
+//               first-order correction -- ~1 ulp f32 phasors at a fraction of the VALU cost.
+//
+// Lane (tl = l&15, h = l>>4) owns time quad tq = 16*chunk + tl (samples 4tq .. 4tq+3) and, in k-step s,
+// antennas 16s + 4h + q (q = 0..3); 16 lanes cover 256 contiguous bytes of an antenna run.
+#include <cstdlib>
+
+#include "bf_mfma.hpp"
+#include "bf_phase.hpp"
+
+namespace bf {
+
+constexpr int kGroup = 4;  // k-steps per register-resident load group (64 antennas)
+
+// Ablation bits for the diagnostic build (tools/diag_fused.py); the product instantiates Mode = 0 only.
+constexpr int kSkipCoef = 1, kSkipMfma = 2, kSkipStore = 4, kSkipLoad = 8;
+
+struct FusedArgs {
+  const uint8_t* raw;
+  const float4* dv;
+  void* y;
+  int delay_channels, B, C, T, A, M, S, NT, nslabs;
+  long long base_ch;
+  double ctot, ts, k, t0, batch_dt;
+  float out_scale;
+};
+
+// One group of 4 k-steps: 16 x 16-byte loads per lane.  Wave-uniform 64-bit base per (step, q) plus one per-lane
+// 32-bit offset keeps the addresses in SGPRs instead of 16 live 64-bit VGPR pairs.
+template <bool Signed>
+__device__ __forceinline__ void load_group(const uint8_t* __restrict__ base, size_t ant_stride, int tq, bool tv,
+                                           int g, int S, int A, int h, uint32_t (&d)[kGroup][4][4]) {
+  const uint32_t lane_off = static_cast<uint32_t>(4 * h * ant_stride) + static_cast<uint32_t>(tq) * 16u;
+#pragma unroll
+  for (int ss = 0; ss < kGroup; ++ss) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int a = 16 * (g + ss) + 4 * h + q;
+      const bool ok = tv && (g + ss) < S && a < A;
+      const uint8_t* bq = base + static_cast<size_t>(16 * (g + ss) + q) * ant_stride;
+      const uint4 v = ok ? *reinterpret_cast<const uint4*>(bq + lane_off) : make_uint4(0, 0, 0, 0);
+      d[ss][q][0] = flip<Signed>(v.x);
+      d[ss][q][1] = flip<Signed>(v.y);
+      d[ss][q][2] = flip<Signed>(v.z);
+      d[ss][q][3] = flip<Signed>(v.w);
+    }
+  }
+}
+
+// Coefficients of item (b, c) for the slab's tiles -> hi/lo fragments in LDS (zero-padded).
+template <bool Exact, int Mode>
+__device__ __forceinline__ void gen_coefs(_Float16* lh, const FusedArgs& P, int b, int c, int tau0, int nts,
+                                          int tid) {
+  const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+  const int cd = P.delay_channels == 1 ? 0 : c;
+  const int nbeam = nts * 8;  // 16 columns per tile = 8 beams
+  const int npairs = P.S * 16 * nbeam;
+  const double ch = static_cast<double>(P.base_ch + c);
+  const double chc = ch - P.ctot / 2.0;
+  for (int e = tid; e < npairs; e += kThreads) {
+    const int a = e / nbeam, ml = e - a * nbeam;
+    const int m = tau0 * 8 + ml;
+    float re = 0.0f, im = 0.0f;
+    if constexpr (Mode & kSkipCoef) {
+      re = 0.5f + 1e-3f * a;
+      im = 0.25f - 1e-3f * m;
+    } else if (a < P.A && m < P.M) {
+      const float4 d = P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a];
+      if constexpr (Exact) {
+        steering_coeff(d, ch, P.ctot, P.ts, dt, &re, &im);
+      } else {
+        steering_coeff_fast(d, chc, P.k, dt, &re, &im);
+      }
+    }
+    const int cl = 2 * ml;
+    put_split(lh, coef_elem(2 * a, cl, nts), re);          // W[2a][2m]     =  cos
+    put_split(lh, coef_elem(2 * a, cl + 1, nts), im);      // W[2a][2m+1]   =  sin
+    put_split(lh, coef_elem(2 * a + 1, cl, nts), -im);     // W[2a+1][2m]   = -sin
+    put_split(lh, coef_elem(2 * a + 1, cl + 1, nts), re);  // W[2a+1][2m+1] =  cos
+  }
+}
+
+// Contract one pol of one group: acc[i][tau] += W^T(s, tau) . X(s, sample 4tq+i, pol p).
+template <bool Signed, int NTS, bool Full>
+__device__ __forceinline__ void contract_pol(const half8* __restrict__ buf, int g, int S, int nts, int lane, int p,
+                                             const uint32_t (&d)[kGroup][4][4], f32x4 (&acc)[4][NTS]) {
+  const uint32_t sel = p ? kSelHi : kSelLo;
+#pragma unroll
+  for (int ss = 0; ss < kGroup; ++ss) {
+    const int s = g + ss;
+    if (s >= S) break;
+    half8 chi[NTS], clo[NTS];
+#pragma unroll
+    for (int tau = 0; tau < NTS; ++tau) {
+      if (Full || tau < nts) {
+        const int slot = ((s * nts + tau) * 2) * 64;
+        chi[tau] = buf[slot + lane];
+        clo[tau] = buf[slot + 64 + lane];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t wv[4] = {pair_to_f16x2<Signed>(d[ss][0][i], sel), pair_to_f16x2<Signed>(d[ss][1][i], sel),
+                              pair_to_f16x2<Signed>(d[ss][2][i], sel), pair_to_f16x2<Signed>(d[ss][3][i], sel)};
+      const half8 v = __builtin_bit_cast(half8, wv);
+#pragma unroll
+      for (int tau = 0; tau < NTS; ++tau) {
+        if (Full || tau < nts) {
+          acc[i][tau] = mfma(chi[tau], v, acc[i][tau]);
+          acc[i][tau] = mfma(clo[tau], v, acc[i][tau]);
+        }
+      }
+    }
+  }
+}
+
+// Store one pol's beams of the 4 samples of quad tq.  Full: every tile complete and 16-byte aligned (2M a
+// multiple of 16*NTS), so each is one unconditional 16-byte (f32) / 4-byte (int8) store.
+template <bool OutI8, int NTS, bool Full>
+__device__ __forceinline__ void store_pol(const FusedArgs& P, int b, int c, int p, int tau0, int nts, int tq, int h,
+                                          const f32x4 (&acc)[4][NTS]) {
+  const int M2 = 2 * P.M;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq + i;
+#pragma unroll
+    for (int tau = 0; tau < NTS; ++tau) {
+      if (Full || tau < nts) {
+        const int col0 = 16 * (tau0 + tau) + 4 * h;
+        if constexpr (OutI8) {
+          int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow * M2;
+          if constexpr (Full) {
+            const uint32_t w = static_cast<uint8_t>(q8(acc[i][tau][0], P.out_scale)) |
+                               (static_cast<uint32_t>(static_cast<uint8_t>(q8(acc[i][tau][1], P.out_scale))) << 8) |
+                               (static_cast<uint32_t>(static_cast<uint8_t>(q8(acc[i][tau][2], P.out_scale))) << 16) |
+                               (static_cast<uint32_t>(static_cast<uint8_t>(q8(acc[i][tau][3], P.out_scale))) << 24);
+            *reinterpret_cast<uint32_t*>(o + col0) = w;
+          } else {
+            store_i8(o, col0, M2, acc[i][tau], P.out_scale);
+          }
+        } else {
+          float* o = reinterpret_cast<float*>(P.y) + orow * M2;
+          if constexpr (Full) {
+            *reinterpret_cast<f32x4*>(o + col0) = acc[i][tau];
+          } else {
+            store_f32<NTS>(o, col0, M2, acc[i][tau]);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Persistent, software-pipelined kernel (A <= 64, T <= 256: one load group, one 64-sample chunk per wave).
+// grid = resident workgroups (2 per CU); workgroup g walks items g, g + grid, ... (item = (slab, b, c), c
+// fastest so concurrently running workgroups read adjacent 1 KiB antenna runs).  Per half-iteration it
+//   1. issues the NEXT item's voltage loads into the other register set,
+//   2. regenerates the NEXT item's coefficients into the other LDS buffer (VALU, under the loads' latency),
+//   3. contracts the CURRENT item on MFMA (one pol at a time) and stores its beams,
+//   4. barriers (LDS hand-over),
+// so HBM reads, coefficient VALU, MFMA and the store stream of different items overlap inside every wave.
+template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
+__global__ __launch_bounds__(kThreads, 2) void beamform_fused_pipe_kernel(FusedArgs P) {
+  extern __shared__ __attribute__((aligned(16))) half8 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const int T4 = P.T >> 2;
+  const int tq = wave * 16 + tl;
+  const bool tv = tq < T4;
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  const int coef_elems = P.S * NTS * 2 * 64;  // half8 per LDS coefficient buffer
+  const int n_items = P.nslabs * P.B * P.C;
+
+  auto split = [&](int item, int& slab, int& b, int& c) {
+    c = item % P.C;
+    const int r = item / P.C;
+    b = r % P.B;
+    slab = r / P.B;
+  };
+  auto prefetch = [&](int item, uint32_t (&d)[kGroup][4][4], half8* buf) {
+    int slab, b, c;
+    split(item, slab, b, c);
+    if constexpr (!(Mode & kSkipLoad)) {
+      const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+      load_group<Signed>(base, ant_stride, tq, tv, 0, P.S, P.A, h, d);
+    }
+    const int tau0 = slab * NTS;
+    gen_coefs<Exact, Mode>(reinterpret_cast<_Float16*>(buf), P, b, c, tau0, Full ? NTS : min(NTS, P.NT - tau0), tid);
+  };
+  auto run = [&](int item, const uint32_t (&d)[kGroup][4][4], const half8* buf) {
+    int slab, b, c;
+    split(item, slab, b, c);
+    const int tau0 = slab * NTS;
+    const int nts = Full ? NTS : min(NTS, P.NT - tau0);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      f32x4 acc[4][NTS];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau) acc[i][tau] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (Mode & kSkipMfma) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][0][q] = __builtin_bit_cast(float, d[q][p + 1][i] ^ d[q][p][i]);
+      } else {
+        contract_pol<Signed, NTS, Full>(buf, 0, P.S, nts, lane, p, d, acc);
+      }
+      if constexpr (Mode & kSkipStore) {
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int tau = 0; tau < NTS; ++tau) sum += acc[i][tau][0] + acc[i][tau][1] + acc[i][tau][2] + acc[i][tau][3];
+        if (sum == 1234.5f) reinterpret_cast<float*>(P.y)[tid] = sum;  // keeps the work alive
+      } else {
+        if (tv) store_pol<OutI8, NTS, Full>(P, b, c, p, tau0, nts, tq, h, acc);
+      }
+    }
+  };
+
+  uint32_t dA[kGroup][4][4], dB[kGroup][4][4];
+  if constexpr (Mode & kSkipLoad) {
+#pragma unroll
+    for (int ss = 0; ss < kGroup; ++ss)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dA[ss][q][j] = dB[ss][q][j] = static_cast<uint32_t>(tid * 0x01010101u + ss + q + j);
+  }
+  half8* bufA = lds;
+  half8* bufB = lds + coef_elems;
+  int item = blockIdx.x;
+  if (item < n_items) prefetch(item, dA, bufA);
+  __syncthreads();
+  while (item < n_items) {
+    int next = item + gridDim.x;
+    if (next < n_items) prefetch(next, dB, bufB);
+    run(item, dA, bufA);
+    __syncthreads();
+    item = next;
+    if (item >= n_items) break;
+    next = item + gridDim.x;
+    if (next < n_items) prefetch(next, dA, bufA);
+    run(item, dB, bufB);
+    __syncthreads();
+    item = next;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Generic kernel: any A (groups of 4 k-steps), any T (chunks of 64 samples per wave).  grid = B*C*nslabs.
+template <bool Signed, bool OutI8, int NTS, bool Exact>
+__global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
+  extern __shared__ __attribute__((aligned(16))) half8 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const int slab = blockIdx.x % P.nslabs;
+  const int bc = blockIdx.x / P.nslabs;
+  const int b = bc / P.C, c = bc % P.C;
+  const int tau0 = slab * NTS;
+  const int nts = min(NTS, P.NT - tau0);
+  const int T4 = P.T >> 2;
+  const int nchunks = (T4 + 15) >> 4;
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+
+  uint32_t d[kGroup][4][4];
+  int chunk = wave;
+  if (chunk < nchunks) load_group<Signed>(base, ant_stride, chunk * 16 + tl, chunk * 16 + tl < T4, 0, P.S, P.A, h, d);
+  gen_coefs<Exact, 0>(reinterpret_cast<_Float16*>(lds), P, b, c, tau0, nts, tid);
+  __syncthreads();
+
+  for (; chunk < nchunks; chunk += kWaves) {
+    const int tq = chunk * 16 + tl;
+    const bool tv = tq < T4;
+    f32x4 acc[2][4][NTS];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau) acc[p][i][tau] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < P.S; g += kGroup) {
+      if (g > 0) load_group<Signed>(base, ant_stride, tq, tv, g, P.S, P.A, h, d);
+      contract_pol<Signed, NTS, false>(lds, g, P.S, nts, lane, 0, d, acc[0]);
+      contract_pol<Signed, NTS, false>(lds, g, P.S, nts, lane, 1, d, acc[1]);
+    }
+    const int next = chunk + kWaves;
+    if (next < nchunks) load_group<Signed>(base, ant_stride, next * 16 + tl, next * 16 + tl < T4, 0, P.S, P.A, h, d);
+    if (tv) {
+      store_pol<OutI8, NTS, false>(P, b, c, 0, tau0, nts, tq, h, acc[0]);
+      store_pol<OutI8, NTS, false>(P, b, c, 1, tau0, nts, tq, h, acc[1]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+inline bool force_generic() {  // BF_FUSED_GENERIC=1: use the generic kernel (tests run both paths)
+  const char* e = getenv("BF_FUSED_GENERIC");
+  return e && e[0] == '1';
+}
+
+template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
+int launch_pipe(FusedArgs P, hipStream_t st) {
+  P.nslabs = (P.NT + NTS - 1) / NTS;
+  const size_t lds = 2 * coef_lds_bytes(P.S, NTS);
+  auto kern = beamform_fused_pipe_kernel<Signed, OutI8, NTS, Exact, Full, Mode>;
+  int dev = 0, cus = 256, per_cu = 2;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds) != hipSuccess) per_cu = 2;
+  per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
+  const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
+  BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many (batch, channel) items");
+  long long grid = static_cast<long long>(cus) * per_cu;
+  if (grid > n_items) grid = n_items;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), lds, st, P);
+  BF_LAUNCHED("beamform_fused_pipe_kernel");
+}
+
+template <bool Signed, bool OutI8, int NTS, bool Exact>
+int launch_generic(FusedArgs P, hipStream_t st) {
+  P.nslabs = (P.NT + NTS - 1) / NTS;
+  const size_t lds = coef_lds_bytes(P.S, NTS);
+  BF_REQUIRE(lds <= kMaxLds, "bf_beamform_fused: n_ants=%d too large", P.A);
+  const long long grid = static_cast<long long>(P.B) * P.C * P.nslabs;
+  BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
+  hipLaunchKernelGGL((beamform_fused_kernel<Signed, OutI8, NTS, Exact>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kThreads), lds, st, P);
+  BF_LAUNCHED("beamform_fused_kernel");
+}
+
+template <bool Signed, bool OutI8, bool Exact>
+int dispatch(FusedArgs P, hipStream_t st) {
+  const bool pipe_ok = P.S <= kGroup && P.T <= 256 &&
+                       static_cast<unsigned long long>(P.C) * P.T * 4 * 64 < (1ULL << 32) && !force_generic();
+  if (pipe_ok) {
+    const int M2 = 2 * P.M;
+    if (P.NT >= 2) {
+      if (M2 % 32 == 0) return launch_pipe<Signed, OutI8, 2, Exact, true>(P, st);
+      return launch_pipe<Signed, OutI8, 2, Exact, false>(P, st);
+    }
+    if (M2 == 16) return launch_pipe<Signed, OutI8, 1, Exact, true>(P, st);
+    return launch_pipe<Signed, OutI8, 1, Exact, false>(P, st);
+  }
+  if (P.NT >= 2 && coef_lds_bytes(P.S, 2) <= kMaxLds) return launch_generic<Signed, OutI8, 2, Exact>(P, st);
+  return launch_generic<Signed, OutI8, 1, Exact>(P, st);
+}
+
+}  // namespace bf
+
+extern "C" int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, int delay_channels, void* y, int B,
+                                 int C, int T, int A, int M, int Ctot, int xeng_id, double sample_period, double t0,
+                                 double batch_dt, int flags, float out_scale, void* stream) {
+  BF_REQUIRE(raw && delay_vals && y, "bf_beamform_fused: null pointer");
+  BF_REQUIRE(B > 0 && C > 0 && T > 0 && A > 0 && M > 0 && Ctot > 0 && xeng_id >= 0,
+             "bf_beamform_fused: bad shape B=%d C=%d T=%d A=%d M=%d Ctot=%d", B, C, T, A, M, Ctot);
+  BF_REQUIRE(T % bf::kSamplesPerBlock == 0, "bf_beamform_fused: n_samples_per_channel=%d must be a multiple of 16", T);
+  BF_REQUIRE(delay_channels == 1 || delay_channels == C, "bf_beamform_fused: delay_channels must be 1 or C");
+  BF_REQUIRE(sample_period > 0.0, "bf_beamform_fused: sample_period must be > 0");
+  BF_REQUIRE((flags & ~(BF_FUSED_SIGNED | BF_FUSED_OUT_INT8 | BF_FUSED_EXACT_COEFF)) == 0,
+             "bf_beamform_fused: unknown flags 0x%x", flags);
+  BF_REQUIRE((reinterpret_cast<uintptr_t>(raw) & 15) == 0 && (reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(y) & 15) == 0,
+             "bf_beamform_fused: misaligned buffer");
+  bf::FusedArgs P{};
+  P.raw = raw;
+  P.dv = reinterpret_cast<const float4*>(delay_vals);
+  P.y = y;
+  P.delay_channels = delay_channels;
+  P.B = B;
+  P.C = C;
+  P.T = T;
+  P.A = A;
+  P.M = M;
+  P.S = (2 * A + 31) / 32;
+  P.NT = (2 * M + 15) / 16;
+  P.base_ch = static_cast<long long>(C) * xeng_id;
+  P.ctot = static_cast<double>(Ctot);
+  P.ts = sample_period;
+  P.k = -3.141592653589793 / (static_cast<double>(Ctot) * sample_period);
+  P.t0 = t0;
+  P.batch_dt = batch_dt;
+  P.out_scale = out_scale;
+  hipStream_t st = bf::as_stream(stream);
+  const bool sgn = flags & BF_FUSED_SIGNED, i8 = flags & BF_FUSED_OUT_INT8, ex = flags & BF_FUSED_EXACT_COEFF;
+  if (sgn) {
+    if (i8) return ex ? bf::dispatch<true, true, true>(P, st) : bf::dispatch<true, true, false>(P, st);
+    return ex ? bf::dispatch<true, false, true>(P, st) : bf::dispatch<true, false, false>(P, st);
+  }
+  if (i8) return ex ? bf::dispatch<false, true, true>(P, st) : bf::dispatch<false, true, false>(P, st);
+  return ex ? bf::dispatch<false, false, true>(P, st) : bf::dispatch<false, false, false>(P, st);
+}
+
+extern "C" double bf_fused_algorithmic_bytes(int B, int C, int T, int A, int M, int delay_channels, int out_int8) {
+  // voltages read once (2 B per complex sample, both pols), beams written once, delay model once.
+  const double samples = static_cast<double>(B) * C * T * 2;  // (b, c, t, p)
+  const double vin = samples * A * 2.0;
+  const double vout = samples * M * 2.0 * (out_int8 ? 1.0 : 4.0);
+  const double dly = static_cast<double>(delay_channels) * M * A * 16.0;
+  return vin + vout + dly;
+}
+
+#ifdef BF_DIAG
+namespace bf {
+// Streams in_bytes in and out_bytes out with 16-byte lanes, `unroll` loads in flight per lane before the stores:
+// the achievable HBM ceiling for the fused kernel's traffic mix.
+template <int U>
+__global__ __launch_bounds__(256) void stream_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n_in,
+                                                     size_t n_out) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const size_t n = n_in > n_out ? n_in : n_out;
+  for (size_t i0 = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i0 < n; i0 += stride * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = i0 + u * stride;
+      v[u] = (i < n_in) ? in[i] : make_uint4(static_cast<uint32_t>(i), 1, 2, 3);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = i0 + u * stride;
+      if (i < n_out) out[i] = v[u];
+    }
+  }
+}
+}  // namespace bf
+
+extern "C" int bf_diag_stream(const void* in, void* out, size_t in_bytes, size_t out_bytes, int grid, int unroll,
+                              void* stream) {
+  auto in4 = reinterpret_cast<const uint4*>(in);
+  auto out4 = reinterpret_cast<uint4*>(out);
+  if (unroll >= 8)
+    hipLaunchKernelGGL(bf::stream_kernel<8>, dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4, in_bytes / 16,
+                       out_bytes / 16);
+  else if (unroll >= 4)
+    hipLaunchKernelGGL(bf::stream_kernel<4>, dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4, in_bytes / 16,
+                       out_bytes / 16);
+  else
+    hipLaunchKernelGGL(bf::stream_kernel<1>, dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4, in_bytes / 16,
+                       out_bytes / 16);
+  BF_LAUNCHED("stream_kernel");
+}
+
+// Ablation of the pipelined kernel (signed input, f32 output, fast coefficients, full tiles): mode = kSkip* bits.
+extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void* y, int B, int C, int T, int A, int M,
+                             int Ctot, double ts, void* stream) {
+  bf::FusedArgs P{};
+  P.raw = raw;
+  P.dv = reinterpret_cast<const float4*>(dv);
+  P.y = y;
+  P.delay_channels = 1;
+  P.B = B;
+  P.C = C;
+  P.T = T;
+  P.A = A;
+  P.M = M;
+  P.S = (2 * A + 31) / 32;
+  P.NT = (2 * M + 15) / 16;
+  P.ctot = Ctot;
+  P.ts = ts;
+  P.k = -3.141592653589793 / (Ctot * ts);
+  P.batch_dt = 1e-3;
+  P.out_scale = 1.0f;
+  hipStream_t st = bf::as_stream(stream);
+  BF_REQUIRE(P.S <= bf::kGroup && T <= 256 && (2 * M) % 32 == 0, "diag: pipelined full-tile shapes only");
+  switch (mode) {
+    case 0: return bf::launch_pipe<true, false, 2, false, true, 0>(P, st);
+    case 1: return bf::launch_pipe<true, false, 2, false, true, 1>(P, st);
+    case 2: return bf::launch_pipe<true, false, 2, false, true, 2>(P, st);
+    case 3: return bf::launch_pipe<true, false, 2, false, true, 3>(P, st);
+    case 4: return bf::launch_pipe<true, false, 2, false, true, 4>(P, st);
+    case 5: return bf::launch_pipe<true, false, 2, false, true, 5>(P, st);
+    case 7: return bf::launch_pipe<true, false, 2, false, true, 7>(P, st);
+    case 8: return bf::launch_pipe<true, false, 2, false, true, 8>(P, st);
+    case 9: return bf::launch_pipe<true, false, 2, false, true, 9>(P, st);
+    case 11: return bf::launch_pipe<true, false, 2, false, true, 11>(P, st);
+    case 16: return bf::launch_pipe<true, false, 2, true, true, 0>(P, st);  // exact coefficients
+    default: bf::set_error("bad mode"); return BF_ERR_ARG;
+  }
+}
+#endif  // BF_DIAG

@@ -35,4 +35,27 @@ __device__ __forceinline__ void steering_coeff(float4 dv, double ch, double ctot
   *im = static_cast<float>(s);
 }
 
+// Fast steering phasor (fused kernels' default): rot = phi' + tau' * (ch - Ctot/2) * K with K = -pi/(Ctot*Ts)
+// precomputed on the host, all in float64 (no divisions, no cancellation), reduced to [-pi, pi] in float64,
+// then a float32 sincos of the reduced angle with a first-order correction for its float32 rounding:
+// |error| ~ 1 ulp of float32 against the exact phasor (the exact mode above is bit-exact to the reference).
+__device__ __forceinline__ void steering_coeff_fast(float4 dv, double chc, double k, double dt, float* re, float* im) {
+  double tau = static_cast<double>(dv.x);
+  double phi = static_cast<double>(dv.z);
+  if (dt != 0.0) {
+    tau = fma(static_cast<double>(dv.y), dt, tau);
+    phi = fma(static_cast<double>(dv.w), dt, phi);
+  }
+  const double rot = fma(tau * chc, k, phi);
+  const double n = rint(rot * 0.15915494309189535);     // 1 / (2 pi)
+  double r = fma(-n, 6.283185307179586, rot);           // 2 pi (hi)
+  r = fma(-n, 2.4492935982947064e-16, r);               // 2 pi (lo)
+  const float rf = static_cast<float>(r);
+  const float dr = static_cast<float>(r - static_cast<double>(rf));
+  float s, c;
+  sincosf(rf, &s, &c);
+  *re = fmaf(-s, dr, c);
+  *im = fmaf(c, dr, s);
+}
+
 }  // namespace bf

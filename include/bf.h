@@ -106,11 +106,15 @@ int bf_beamform(const uint8_t* x, const float* w, float* y, int B, int P, int C,
  *   raw        : 8-bit (B, A, C, T, 2, 2), the reorder's input layout, read directly
  *   delay_vals : f32 (Cd, M, A, 4), Cd = C or 1; batch b uses dt_b = t0 + b*batch_dt (regeneration per
  *                block of T samples, BeamformerParameters.h:17); with zero rates/dt it equals OpSequence
- *   y          : out_int8 = 0 -> f32 (B, 2, C, T/16, 16, 2M);
- *                out_int8 = 1 -> int8 (B, 2, C, T/16, 16, 2M) = sat127(rne(y * out_scale)) (bf_requant). */
+ *   y          : f32 (B, 2, C, T/16, 16, 2M), or int8 = sat127(rne(y * out_scale)) with BF_FUSED_OUT_INT8
+ *   flags      : BF_FUSED_SIGNED (int8 samples), BF_FUSED_OUT_INT8, BF_FUSED_EXACT_COEFF (float64 phasors
+ *                bit-exact to bf_coeff_gen; default is the ~1-ulp float32 fast phasor). */
+#define BF_FUSED_SIGNED 1
+#define BF_FUSED_OUT_INT8 2
+#define BF_FUSED_EXACT_COEFF 4
 int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, int delay_channels, void* y, int B, int C,
                       int T, int A, int M, int Ctot, int xeng_id, double sample_period, double t0,
-                      double batch_dt, int sample_signed, int out_int8, float out_scale, void* stream);
+                      double batch_dt, int flags, float out_scale, void* stream);
 
 /* 8-bit requantiser (no reference counterpart; SURVEY §7 build step 7): q = clamp(rne(y*scale), -127, 127). */
 int bf_requant(const float* y, int8_t* q, size_t n, float scale, void* stream);

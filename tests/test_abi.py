@@ -53,12 +53,13 @@ def test_argument_validation_without_gpu():
     with pytest.raises(_lib.BeamformerError, match="bad shape"):
         _lib.call("bf_beamform", fake, fake, fake, 0, 2, 1, 1, 4, 1, 0, None)
     with pytest.raises(_lib.BeamformerError, match="delay_channels"):
-        _lib.call("bf_beamform_fused", fake, fake, 3, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0, 0, 0, 1.0, None)
+        _lib.call("bf_beamform_fused", fake, fake, 3, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0, 0, 1.0, None)
     with pytest.raises(_lib.BeamformerError, match="null pointer"):
         _lib.call("bf_coeff_gen", None, None, 1, 1, 1, 1, 1, 1, 0, 1e-9, None)
     with pytest.raises(_lib.BeamformerError, match="misaligned"):
-        _lib.call("bf_beamform_fused", fake + 1, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0, 0, 0, 1.0,
-                  None)
+        _lib.call("bf_beamform_fused", fake + 1, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0, 0, 1.0, None)
+    with pytest.raises(_lib.BeamformerError, match="unknown flags"):
+        _lib.call("bf_beamform_fused", fake, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0, 64, 1.0, None)
 
 
 def test_algorithmic_bytes():

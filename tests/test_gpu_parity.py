@@ -233,7 +233,7 @@ def test_beamform_op_sequence(context, command_queue, n_batches, n_ants, n_chann
 
 
 # ---- fused one-pass operator --------------------------------------------------------------------------------
-def test_fused_equals_op_sequence_bitwise(context, command_queue):
+def test_fused_equals_op_sequence_bitwise(context, command_queue, fused_path):
     """Same coefficients (float64 phase), same fragment order, same accumulation: identical bits."""
     B, A, M, C, Ctot, T = 2, 64, 16, 8, 4096, 256
     d = random_delays(C, M, A, 11, rates=False)
@@ -244,18 +244,32 @@ def test_fused_equals_op_sequence_bitwise(context, command_queue):
     seq.prebeamform_reorder.buffer("inSamples").set(command_queue, raw)
     seq()
     y_seq = seq.beamform_mult.buffer("outData").get(command_queue)
-    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=2, sample_period=TS).instantiate(command_queue)
+    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=2, sample_period=TS,
+                                 exact_coeffs=True).instantiate(command_queue)
     (y_fu,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     np.testing.assert_array_equal(y_fu, y_seq)
     assert_beams_allclose(y_fu, O.op_sequence(raw, d, C, Ctot, A, M, xeng_id=2), O.reorder(raw),
                           O.coeffs(d, B, 2, C, Ctot, A, M, 2))
 
 
+@pytest.fixture(params=["pipelined", "generic"])
+def fused_path(request, monkeypatch):
+    """Run a fused test through the persistent pipelined kernel (default for A <= 64, T <= 256) and through the
+    generic kernel (BF_FUSED_GENERIC=1, what larger shapes use)."""
+    if request.param == "generic":
+        monkeypatch.setenv("BF_FUSED_GENERIC", "1")
+    else:
+        monkeypatch.delenv("BF_FUSED_GENERIC", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
     (64, 16, 4, 256, 3, 1, True), (64, 1, 4, 256, 2, 4, False), (4, 1, 64, 1024, 1, 64, False),
     (19, 2, 13, 256, 3, 1, False), (5, 3, 7, 48, 2, 7, True), (130, 9, 2, 64, 2, 1, False),
-    (256, 64, 1, 32, 1, 1, True), (80, 2, 3, 16, 3, 3, False)])
-def test_fused_matches_oracle(context, command_queue, A, M, C, T, B, dch, signed):
+    (256, 64, 1, 32, 1, 1, True), (80, 2, 3, 16, 3, 3, False), (64, 16, 700, 256, 2, 1, False),
+    (32, 24, 9, 128, 5, 9, True)])
+@pytest.mark.parametrize("exact", [False, True])
+def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C, T, B, dch, signed):
     Ctot, xeng = 8192, 3
     d = random_delays(dch, M, A, A * 31 + M)
     rng = np.random.default_rng(A + M + C)
@@ -264,14 +278,15 @@ def test_fused_matches_oracle(context, command_queue, A, M, C, T, B, dch, signed
         raw = raw.view(np.int8)
     t0, bdt = 2.5e-3, 256 * 8192 * TS
     fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, sample_period=TS, delay_channels=dch,
-                                 sample_signed=signed, t0=t0, batch_dt=bdt).instantiate(command_queue)
+                                 sample_signed=signed, t0=t0, batch_dt=bdt, exact_coeffs=exact).instantiate(
+                                     command_queue)
     (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     ref = O.fused_beamform(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, signed=signed)
     w = O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, t0=t0, batch_dt=bdt)
     assert_beams_allclose(y, ref, O.reorder(raw), w, signed=signed)
 
 
-def test_fused_int8_output_is_requantised_f32(context, command_queue):
+def test_fused_int8_output_is_requantised_f32(context, command_queue, fused_path):
     B, A, M, C, T, Ctot = 2, 64, 16, 4, 256, 4096
     d = random_delays(1, M, A, 9)
     raw = O.u8_voltages((B, A, C, T, 2, 2), seed=9).view(np.int8)

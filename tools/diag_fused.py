@@ -1,0 +1,51 @@
+"""Ablation timing of the fused kernel (diagnostic library build/libbf_diag.so) + HBM stream ceilings.
+
+Modes: 1 skip coefficient generation, 2 skip MFMA (cheap VALU reduction instead), 4 skip stores,
+8 skip loads (synthetic registers).  Times are HIP-event averages over N launches, 2 rotating buffer sets."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np
+from dpdk_dc_sand_amd import _lib, accel
+
+lib = _lib.load(os.path.join(ROOT, "build", "libbf_diag.so"))
+V, I, D, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
+lib.bf_diag_fused.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
+lib.bf_diag_stream.argtypes = [V, V, S, S, I, I, V]
+ctx = accel.create_some_context()
+q = ctx.create_command_queue()
+B, C, T, A, M = [int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (8, 4096, 256, 64, 16))]
+nin = B * A * C * T * 4
+nout = B * 2 * C * T * 2 * M * 4
+bufs = [(accel.DeviceArray(ctx, (nin,), np.uint8), accel.DeviceArray(ctx, (nout,), np.uint8)) for _ in range(2)]
+for xi, yo in bufs:
+    _lib.call("bf_memset", xi.ptr, 7, nin, q.handle)
+dv = accel.DeviceArray(ctx, (M * A * 4,), np.float32)
+dv.set(q, np.random.default_rng(0).uniform(0, 1e-8, M * A * 4).astype(np.float32))
+alg = nin + nout
+
+
+def timeit(fn, n=20):
+    for i in range(3):
+        fn(i)
+    e0, e1 = accel.Event(), accel.Event()
+    q.finish(); e0.record(q)
+    for i in range(n):
+        fn(i)
+    e1.record(q); q.finish()
+    return e1.time_since(e0) / n
+
+
+names = {0: "full (fast coef)", 16: "full (exact coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
+         3: "no-coef,no-mfma", 5: "no-coef,no-store", 9: "no-coef,no-load", 7: "loads only", 11: "stores only"}
+print(f"shape B={B} C={C} T={T} A={A} M={M}: in {nin/2**30:.2f} GiB out {nout/2**30:.2f} GiB")
+for mode, name in names.items():
+    t = timeit(lambda i: lib.bf_diag_fused(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr, B, C, T, A, M, C,
+                                           1 / 1712e6, q.handle))
+    print(f"  mode {mode:2d} {name:18s} {t*1e6:9.1f} us   alg {alg/t/1e9:7.1f} GB/s")
+for grid in (1024, 2048, 8192):
+    for unroll in (1, 4, 8):
+        for (ri, wo, nm) in ((nin, nout, "read+write"), (nin, 0, "read only"), (0, nout, "write only")):
+            t = timeit(lambda i: lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, ri, wo, grid, unroll,
+                                                    q.handle))
+            print(f"  stream grid {grid:5d} unroll {unroll} {nm:11s} {t*1e6:8.1f} us  {(ri + wo)/t/1e9:7.1f} GB/s")
