@@ -233,7 +233,7 @@ def main():
         "device": r["device"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "beamform_fused_kernel", "avg_launch_us": round(r["kernel_s"] * 1e6, 2),
+                     "kernel": "beamform_fused_item_kernel", "avg_launch_us": round(r["kernel_s"] * 1e6, 2),
                      "alg_bytes_per_launch": r["alg_bytes"]},
         "cpu_baseline": None,
     }

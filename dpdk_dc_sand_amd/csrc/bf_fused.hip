@@ -39,39 +39,78 @@ struct FusedArgs {
   float out_scale;
 };
 
-// One group of 4 k-steps: 16 x 16-byte loads per lane.  Wave-uniform 64-bit base per (step, q) plus one per-lane
-// 32-bit offset keeps the addresses in SGPRs instead of 16 live 64-bit VGPR pairs.
-template <bool Signed>
-__device__ __forceinline__ void load_group(const uint8_t* __restrict__ base, size_t ant_stride, int tq, bool tv,
-                                           int g, int S, int A, int h, uint32_t (&d)[kGroup][4][4]) {
-  const uint32_t lane_off = static_cast<uint32_t>(4 * h * ant_stride) + static_cast<uint32_t>(tq) * 16u;
+// One group of 4 k-steps: 16 x 16-byte loads per lane, all UNCONDITIONAL: out-of-range antennas (a >= A) read
+// antenna A-1 and meet zero coefficient rows, out-of-range time quads read the last quad and are never stored,
+// steps s >= S are never contracted.  (A predicated load makes hipcc branch around it and wait vmcnt(0) right
+// after it, serialising the group.)  Wave-uniform 64-bit base per (step, q) plus one per-lane 32-bit offset
+// keeps the addresses in SGPRs.  Raw bytes are kept; the signed-sample flip happens at the consumer.
+__device__ __forceinline__ void load_group(const uint8_t* __restrict__ base, size_t ant_stride, int tq, int T4, int g,
+                                           int A, int h, uint32_t (&d)[kGroup][4][4]) {
+  const int tqc = tq < T4 ? tq : T4 - 1;
 #pragma unroll
   for (int ss = 0; ss < kGroup; ++ss) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int a = 16 * (g + ss) + 4 * h + q;
-      const bool ok = tv && (g + ss) < S && a < A;
-      const uint8_t* bq = base + static_cast<size_t>(16 * (g + ss) + q) * ant_stride;
-      const uint4 v = ok ? *reinterpret_cast<const uint4*>(bq + lane_off) : make_uint4(0, 0, 0, 0);
-      d[ss][q][0] = flip<Signed>(v.x);
-      d[ss][q][1] = flip<Signed>(v.y);
-      d[ss][q][2] = flip<Signed>(v.z);
-      d[ss][q][3] = flip<Signed>(v.w);
+      int a = 16 * (g + ss) + 4 * h + q;
+      a = a < A ? a : A - 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(base + static_cast<size_t>(a) * ant_stride +
+                                                      static_cast<uint32_t>(tqc) * 16u);
+      d[ss][q][0] = v.x;
+      d[ss][q][1] = v.y;
+      d[ss][q][2] = v.z;
+      d[ss][q][3] = v.w;
     }
   }
 }
 
-// Coefficients of item (b, c) for the slab's tiles -> hi/lo fragments in LDS (zero-padded).
-template <bool Exact, int Mode>
-__device__ __forceinline__ void gen_coefs(_Float16* lh, const FusedArgs& P, int b, int c, int tau0, int nts,
-                                          int tid) {
-  const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+template <bool Signed>
+__device__ __forceinline__ void flip_group(uint32_t (&d)[kGroup][4][4]) {
+  if constexpr (Signed) {
+#pragma unroll
+    for (int ss = 0; ss < kGroup; ++ss)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[ss][q][j] ^= 0x80808080u;
+  }
+}
+
+// Coefficients of item (b, c) for the slab's tiles -> hi/lo fragments in LDS (zero-padded), in two parts so the
+// delay-model loads can be issued BEFORE the item's voltage loads (vmcnt counts in order: a load issued after the
+// voltages could only be waited for by draining them too).  Pair e = tid + j*kThreads, j < kMaxPairs.
+template <int NTS>
+struct CoefPrefetch {
+  static constexpr int kMaxPairs = (kGroup * 16 * 8 * NTS) / kThreads;  // S <= 4
+  float4 dv[kMaxPairs];
+};
+
+template <int NTS>
+__device__ __forceinline__ void load_delays(CoefPrefetch<NTS>& cp, const FusedArgs& P, int c, int tau0, int nts,
+                                            int tid) {
   const int cd = P.delay_channels == 1 ? 0 : c;
-  const int nbeam = nts * 8;  // 16 columns per tile = 8 beams
+  const int nbeam = nts * 8;
+#pragma unroll
+  for (int j = 0; j < CoefPrefetch<NTS>::kMaxPairs; ++j) {
+    const int e = tid + j * kThreads;
+    int a = e / nbeam, m = tau0 * 8 + (e - (e / nbeam) * nbeam);
+    a = a < P.A ? a : P.A - 1;
+    m = m < P.M ? m : P.M - 1;
+    cp.dv[j] = P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a];
+  }
+}
+
+template <bool Exact, int Mode, int NTS>
+__device__ __forceinline__ void make_coefs(_Float16* lh, const CoefPrefetch<NTS>& cp, const FusedArgs& P, int b, int c,
+                                           int tau0, int nts, int tid) {
+  const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+  const int nbeam = nts * 8;
   const int npairs = P.S * 16 * nbeam;
   const double ch = static_cast<double>(P.base_ch + c);
   const double chc = ch - P.ctot / 2.0;
-  for (int e = tid; e < npairs; e += kThreads) {
+#pragma unroll
+  for (int j = 0; j < CoefPrefetch<NTS>::kMaxPairs; ++j) {
+    const int e = tid + j * kThreads;
+    if (e >= npairs) break;
     const int a = e / nbeam, ml = e - a * nbeam;
     const int m = tau0 * 8 + ml;
     float re = 0.0f, im = 0.0f;
@@ -79,6 +118,35 @@ __device__ __forceinline__ void gen_coefs(_Float16* lh, const FusedArgs& P, int 
       re = 0.5f + 1e-3f * a;
       im = 0.25f - 1e-3f * m;
     } else if (a < P.A && m < P.M) {
+      if constexpr (Exact) {
+        steering_coeff(cp.dv[j], ch, P.ctot, P.ts, dt, &re, &im);
+      } else {
+        steering_coeff_fast(cp.dv[j], chc, P.k, dt, &re, &im);
+      }
+    }
+    const int cl = 2 * ml;
+    put_split(lh, coef_elem(2 * a, cl, nts), re);          // W[2a][2m]     =  cos
+    put_split(lh, coef_elem(2 * a, cl + 1, nts), im);      // W[2a][2m+1]   =  sin
+    put_split(lh, coef_elem(2 * a + 1, cl, nts), -im);     // W[2a+1][2m]   = -sin
+    put_split(lh, coef_elem(2 * a + 1, cl + 1, nts), re);  // W[2a+1][2m+1] =  cos
+  }
+}
+
+// Generic-kernel form (any S): straight loop, loads inline.
+template <bool Exact>
+__device__ __forceinline__ void gen_coefs(_Float16* lh, const FusedArgs& P, int b, int c, int tau0, int nts,
+                                          int tid) {
+  const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+  const int cd = P.delay_channels == 1 ? 0 : c;
+  const int nbeam = nts * 8;
+  const int npairs = P.S * 16 * nbeam;
+  const double ch = static_cast<double>(P.base_ch + c);
+  const double chc = ch - P.ctot / 2.0;
+  for (int e = tid; e < npairs; e += kThreads) {
+    const int a = e / nbeam, ml = e - a * nbeam;
+    const int m = tau0 * 8 + ml;
+    float re = 0.0f, im = 0.0f;
+    if (a < P.A && m < P.M) {
       const float4 d = P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a];
       if constexpr (Exact) {
         steering_coeff(d, ch, P.ctot, P.ts, dt, &re, &im);
@@ -87,10 +155,10 @@ __device__ __forceinline__ void gen_coefs(_Float16* lh, const FusedArgs& P, int 
       }
     }
     const int cl = 2 * ml;
-    put_split(lh, coef_elem(2 * a, cl, nts), re);          // W[2a][2m]     =  cos
-    put_split(lh, coef_elem(2 * a, cl + 1, nts), im);      // W[2a][2m+1]   =  sin
-    put_split(lh, coef_elem(2 * a + 1, cl, nts), -im);     // W[2a+1][2m]   = -sin
-    put_split(lh, coef_elem(2 * a + 1, cl + 1, nts), re);  // W[2a+1][2m+1] =  cos
+    put_split(lh, coef_elem(2 * a, cl, nts), re);
+    put_split(lh, coef_elem(2 * a, cl + 1, nts), im);
+    put_split(lh, coef_elem(2 * a + 1, cl, nts), -im);
+    put_split(lh, coef_elem(2 * a + 1, cl + 1, nts), re);
   }
 }
 
@@ -195,16 +263,22 @@ __global__ __launch_bounds__(kThreads, 2) void beamform_fused_pipe_kernel(FusedA
   auto prefetch = [&](int item, uint32_t (&d)[kGroup][4][4], half8* buf) {
     int slab, b, c;
     split(item, slab, b, c);
-    if constexpr (!(Mode & kSkipLoad)) {
-      const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
-      load_group<Signed>(base, ant_stride, tq, tv, 0, P.S, P.A, h, d);
-    }
     const int tau0 = slab * NTS;
-    gen_coefs<Exact, Mode>(reinterpret_cast<_Float16*>(buf), P, b, c, tau0, Full ? NTS : min(NTS, P.NT - tau0), tid);
+    const int nts = Full ? NTS : min(NTS, P.NT - tau0);
+    CoefPrefetch<NTS> cp;
+    if constexpr (!(Mode & kSkipCoef)) load_delays<NTS>(cp, P, c, tau0, nts, tid);  // 1. delay model (oldest)
+    __builtin_amdgcn_sched_barrier(0);  // keep the issue order: waiting for the delays must not drain the voltages
+    if constexpr (!(Mode & kSkipLoad)) {                                             // 2. voltages
+      const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+      load_group(base, ant_stride, tq, T4, 0, P.A, h, d);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    make_coefs<Exact, Mode, NTS>(reinterpret_cast<_Float16*>(buf), cp, P, b, c, tau0, nts, tid);  // 3. under them
   };
-  auto run = [&](int item, const uint32_t (&d)[kGroup][4][4], const half8* buf) {
+  auto run = [&](int item, uint32_t (&d)[kGroup][4][4], const half8* buf) {
     int slab, b, c;
     split(item, slab, b, c);
+    flip_group<Signed>(d);
     const int tau0 = slab * NTS;
     const int nts = Full ? NTS : min(NTS, P.NT - tau0);
 #pragma unroll
@@ -265,6 +339,74 @@ __global__ __launch_bounds__(kThreads, 2) void beamform_fused_pipe_kernel(FusedA
 }
 
 // ---------------------------------------------------------------------------------------------------------
+// Single-item kernel (A <= 64, T <= 256): grid = items, one (slab, b, c) per workgroup, one register set.
+// Issue order delay model -> voltages (16 x 16 B per lane, all in flight) -> coefficient math under them ->
+// barrier -> per pol: MFMA contraction + stores.  Memory/compute overlap comes from the 3+ workgroups a CU holds
+// at this register footprint (the hardware interleaves their phases).
+template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
+__global__ __launch_bounds__(kThreads) void beamform_fused_item_kernel(FusedArgs P) {
+  extern __shared__ __attribute__((aligned(16))) half8 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const int T4 = P.T >> 2;
+  const int tq = wave * 16 + tl;
+  const bool tv = tq < T4;
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  const int item = blockIdx.x;
+  const int c = item % P.C;
+  const int b = (item / P.C) % P.B;
+  const int slab = item / (P.C * P.B);
+  const int tau0 = slab * NTS;
+  const int nts = Full ? NTS : min(NTS, P.NT - tau0);
+
+  uint32_t d[kGroup][4][4];
+  CoefPrefetch<NTS> cp;
+  if constexpr (!(Mode & kSkipCoef)) load_delays<NTS>(cp, P, c, tau0, nts, tid);
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (Mode & kSkipLoad) {
+#pragma unroll
+    for (int ss = 0; ss < kGroup; ++ss)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[ss][q][j] = static_cast<uint32_t>(tid * 0x01010101u + ss + q + j);
+  } else {
+    const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+    load_group(base, ant_stride, tq, T4, 0, P.A, h, d);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  make_coefs<Exact, Mode, NTS>(reinterpret_cast<_Float16*>(lds), cp, P, b, c, tau0, nts, tid);
+  __syncthreads();
+  flip_group<Signed>(d);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    f32x4 acc[4][NTS];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int tau = 0; tau < NTS; ++tau) acc[i][tau] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (Mode & kSkipMfma) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][0][q] = __builtin_bit_cast(float, d[q][p + 1][i] ^ d[q][p][i]);
+    } else {
+      contract_pol<Signed, NTS, Full>(lds, 0, P.S, nts, lane, p, d, acc);
+    }
+    if constexpr (Mode & kSkipStore) {
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau) sum += acc[i][tau][0] + acc[i][tau][1] + acc[i][tau][2] + acc[i][tau][3];
+      if (sum == 1234.5f) reinterpret_cast<float*>(P.y)[tid] = sum;
+    } else {
+      if (tv) store_pol<OutI8, NTS, Full>(P, b, c, p, tau0, nts, tq, h, acc);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
 // Generic kernel: any A (groups of 4 k-steps), any T (chunks of 64 samples per wave).  grid = B*C*nslabs.
 template <bool Signed, bool OutI8, int NTS, bool Exact>
 __global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
@@ -283,8 +425,18 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
 
   uint32_t d[kGroup][4][4];
   int chunk = wave;
-  if (chunk < nchunks) load_group<Signed>(base, ant_stride, chunk * 16 + tl, chunk * 16 + tl < T4, 0, P.S, P.A, h, d);
-  gen_coefs<Exact, 0>(reinterpret_cast<_Float16*>(lds), P, b, c, tau0, nts, tid);
+  if (P.S <= kGroup) {
+    // delay model, then voltages, then the coefficient math under the voltage loads (issue order pinned)
+    CoefPrefetch<NTS> cp;
+    load_delays<NTS>(cp, P, c, tau0, nts, tid);
+    __builtin_amdgcn_sched_barrier(0);
+    if (chunk < nchunks) load_group(base, ant_stride, chunk * 16 + tl, T4, 0, P.A, h, d);
+    __builtin_amdgcn_sched_barrier(0);
+    make_coefs<Exact, 0, NTS>(reinterpret_cast<_Float16*>(lds), cp, P, b, c, tau0, nts, tid);
+  } else {
+    if (chunk < nchunks) load_group(base, ant_stride, chunk * 16 + tl, T4, 0, P.A, h, d);
+    gen_coefs<Exact>(reinterpret_cast<_Float16*>(lds), P, b, c, tau0, nts, tid);
+  }
   __syncthreads();
 
   for (; chunk < nchunks; chunk += kWaves) {
@@ -298,12 +450,13 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
 #pragma unroll
         for (int tau = 0; tau < NTS; ++tau) acc[p][i][tau] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int g = 0; g < P.S; g += kGroup) {
-      if (g > 0) load_group<Signed>(base, ant_stride, tq, tv, g, P.S, P.A, h, d);
+      if (g > 0) load_group(base, ant_stride, tq, T4, g, P.A, h, d);
+      flip_group<Signed>(d);
       contract_pol<Signed, NTS, false>(lds, g, P.S, nts, lane, 0, d, acc[0]);
       contract_pol<Signed, NTS, false>(lds, g, P.S, nts, lane, 1, d, acc[1]);
     }
     const int next = chunk + kWaves;
-    if (next < nchunks) load_group<Signed>(base, ant_stride, next * 16 + tl, next * 16 + tl < T4, 0, P.S, P.A, h, d);
+    if (next < nchunks) load_group(base, ant_stride, next * 16 + tl, T4, 0, P.A, h, d);
     if (tv) {
       store_pol<OutI8, NTS, false>(P, b, c, 0, tau0, nts, tq, h, acc[0]);
       store_pol<OutI8, NTS, false>(P, b, c, 1, tau0, nts, tq, h, acc[1]);
@@ -312,9 +465,16 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
 }
 
 // ---------------------------------------------------------------------------------------------------------
-inline bool force_generic() {  // BF_FUSED_GENERIC=1: use the generic kernel (tests run both paths)
-  const char* e = getenv("BF_FUSED_GENERIC");
-  return e && e[0] == '1';
+// Kernel choice for A <= 64, T <= 256: BF_FUSED_KERNEL = item (default) | pipe | generic; BF_FUSED_GENERIC=1 is
+// shorthand for generic (tests run every path against the oracle).
+inline int fused_kernel_choice() {
+  const char* g = getenv("BF_FUSED_GENERIC");
+  if (g && g[0] == '1') return 2;
+  const char* e = getenv("BF_FUSED_KERNEL");
+  if (!e) return 0;
+  if (e[0] == 'p') return 1;
+  if (e[0] == 'g') return 2;
+  return 0;
 }
 
 template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
@@ -336,6 +496,17 @@ int launch_pipe(FusedArgs P, hipStream_t st) {
   BF_LAUNCHED("beamform_fused_pipe_kernel");
 }
 
+template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
+int launch_item(FusedArgs P, hipStream_t st) {
+  P.nslabs = (P.NT + NTS - 1) / NTS;
+  const size_t lds = coef_lds_bytes(P.S, NTS);
+  const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
+  BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many (batch, channel) items");
+  hipLaunchKernelGGL((beamform_fused_item_kernel<Signed, OutI8, NTS, Exact, Full, Mode>),
+                     dim3(static_cast<unsigned>(n_items)), dim3(kThreads), lds, st, P);
+  BF_LAUNCHED("beamform_fused_item_kernel");
+}
+
 template <bool Signed, bool OutI8, int NTS, bool Exact>
 int launch_generic(FusedArgs P, hipStream_t st) {
   P.nslabs = (P.NT + NTS - 1) / NTS;
@@ -350,16 +521,24 @@ int launch_generic(FusedArgs P, hipStream_t st) {
 
 template <bool Signed, bool OutI8, bool Exact>
 int dispatch(FusedArgs P, hipStream_t st) {
-  const bool pipe_ok = P.S <= kGroup && P.T <= 256 &&
-                       static_cast<unsigned long long>(P.C) * P.T * 4 * 64 < (1ULL << 32) && !force_generic();
-  if (pipe_ok) {
+  const int choice = fused_kernel_choice();
+  const bool small = P.S <= kGroup && P.T <= 256;
+  if (small && choice != 2) {
     const int M2 = 2 * P.M;
-    if (P.NT >= 2) {
-      if (M2 % 32 == 0) return launch_pipe<Signed, OutI8, 2, Exact, true>(P, st);
-      return launch_pipe<Signed, OutI8, 2, Exact, false>(P, st);
+    if (choice == 1) {
+      if (P.NT >= 2) {
+        if (M2 % 32 == 0) return launch_pipe<Signed, OutI8, 2, Exact, true>(P, st);
+        return launch_pipe<Signed, OutI8, 2, Exact, false>(P, st);
+      }
+      if (M2 == 16) return launch_pipe<Signed, OutI8, 1, Exact, true>(P, st);
+      return launch_pipe<Signed, OutI8, 1, Exact, false>(P, st);
     }
-    if (M2 == 16) return launch_pipe<Signed, OutI8, 1, Exact, true>(P, st);
-    return launch_pipe<Signed, OutI8, 1, Exact, false>(P, st);
+    if (P.NT >= 2) {
+      if (M2 % 32 == 0) return launch_item<Signed, OutI8, 2, Exact, true>(P, st);
+      return launch_item<Signed, OutI8, 2, Exact, false>(P, st);
+    }
+    if (M2 == 16) return launch_item<Signed, OutI8, 1, Exact, true>(P, st);
+    return launch_item<Signed, OutI8, 1, Exact, false>(P, st);
   }
   if (P.NT >= 2 && coef_lds_bytes(P.S, 2) <= kMaxLds) return launch_generic<Signed, OutI8, 2, Exact>(P, st);
   return launch_generic<Signed, OutI8, 1, Exact>(P, st);
@@ -482,6 +661,22 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
   P.out_scale = 1.0f;
   hipStream_t st = bf::as_stream(stream);
   BF_REQUIRE(P.S <= bf::kGroup && T <= 256 && (2 * M) % 32 == 0, "diag: pipelined full-tile shapes only");
+  if (mode >= 32) {
+    switch (mode - 32) {
+      case 0: return bf::launch_item<true, false, 2, false, true, 0>(P, st);
+      case 1: return bf::launch_item<true, false, 2, false, true, 1>(P, st);
+      case 2: return bf::launch_item<true, false, 2, false, true, 2>(P, st);
+      case 3: return bf::launch_item<true, false, 2, false, true, 3>(P, st);
+      case 4: return bf::launch_item<true, false, 2, false, true, 4>(P, st);
+      case 5: return bf::launch_item<true, false, 2, false, true, 5>(P, st);
+      case 7: return bf::launch_item<true, false, 2, false, true, 7>(P, st);
+      case 8: return bf::launch_item<true, false, 2, false, true, 8>(P, st);
+      case 9: return bf::launch_item<true, false, 2, false, true, 9>(P, st);
+      case 11: return bf::launch_item<true, false, 2, false, true, 11>(P, st);
+      case 16: return bf::launch_item<true, false, 2, true, true, 0>(P, st);
+      default: bf::set_error("bad mode"); return BF_ERR_ARG;
+    }
+  }
   switch (mode) {
     case 0: return bf::launch_pipe<true, false, 2, false, true, 0>(P, st);
     case 1: return bf::launch_pipe<true, false, 2, false, true, 1>(P, st);

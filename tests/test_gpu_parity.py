@@ -252,14 +252,12 @@ def test_fused_equals_op_sequence_bitwise(context, command_queue, fused_path):
                           O.coeffs(d, B, 2, C, Ctot, A, M, 2))
 
 
-@pytest.fixture(params=["pipelined", "generic"])
+@pytest.fixture(params=["item", "pipe", "generic"])
 def fused_path(request, monkeypatch):
-    """Run a fused test through the persistent pipelined kernel (default for A <= 64, T <= 256) and through the
-    generic kernel (BF_FUSED_GENERIC=1, what larger shapes use)."""
-    if request.param == "generic":
-        monkeypatch.setenv("BF_FUSED_GENERIC", "1")
-    else:
-        monkeypatch.delenv("BF_FUSED_GENERIC", raising=False)
+    """Run a fused test through each kernel: the single-item kernel (default for A <= 64, T <= 256), the
+    persistent pipelined kernel, and the generic kernel (what larger shapes use)."""
+    monkeypatch.delenv("BF_FUSED_GENERIC", raising=False)
+    monkeypatch.setenv("BF_FUSED_KERNEL", request.param)
     return request.param
 
 

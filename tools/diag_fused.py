@@ -39,10 +39,11 @@ def timeit(fn, n=20):
 names = {0: "full (fast coef)", 16: "full (exact coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
          3: "no-coef,no-mfma", 5: "no-coef,no-store", 9: "no-coef,no-load", 7: "loads only", 11: "stores only"}
 print(f"shape B={B} C={C} T={T} A={A} M={M}: in {nin/2**30:.2f} GiB out {nout/2**30:.2f} GiB")
-for mode, name in names.items():
-    t = timeit(lambda i: lib.bf_diag_fused(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr, B, C, T, A, M, C,
-                                           1 / 1712e6, q.handle))
-    print(f"  mode {mode:2d} {name:18s} {t*1e6:9.1f} us   alg {alg/t/1e9:7.1f} GB/s")
+for kbase, kname in ((0, "pipe"), (32, "item")):
+    for mode, name in names.items():
+        t = timeit(lambda i: lib.bf_diag_fused(kbase + mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr, B, C, T,
+                                               A, M, C, 1 / 1712e6, q.handle))
+        print(f"  {kname} mode {mode:2d} {name:18s} {t*1e6:9.1f} us   alg {alg/t/1e9:7.1f} GB/s")
 for grid in (1024, 2048, 8192):
     for unroll in (1, 4, 8):
         for (ri, wo, nm) in ((nin, nout, "read+write"), (nin, 0, "read only"), (0, nout, "write only")):

@@ -16,4 +16,4 @@ for s in $STAGES; do
   esac
   echo "stage $s ok"
 done
-cat $OUT/bench.json 2>/dev/null
+[ -f $OUT/bench.json ] && cat $OUT/bench.json; true
