@@ -68,7 +68,15 @@ class Dist:
         if self.world > 1:
             import torch.distributed as dist  # imported before libbf so one HIP runtime serves both
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            saved = os.dup(1)  # gloo prints its connection banner on stdout: keep stdout for the JSON line
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+                dist.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):

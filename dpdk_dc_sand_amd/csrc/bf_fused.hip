@@ -28,6 +28,11 @@ constexpr int kGroup = 4;  // k-steps per register-resident load group (64 anten
 
 // Ablation bits for the diagnostic build (tools/diag_fused.py); the product instantiates Mode = 0 only.
 constexpr int kSkipCoef = 1, kSkipMfma = 2, kSkipStore = 4, kSkipLoad = 8;
+// Cache-policy bits for measurement: the product streams voltages with non-temporal loads (read once: -1.8 %
+// time, profiles/r1_v2_ablation_nt.txt); kCachedLoad selects plain loads, kNtStore non-temporal beam stores
+// (slower: +17 %).
+constexpr int kCachedLoad = 128, kNtStore = 256;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 struct FusedArgs {
   const uint8_t* raw;
@@ -44,6 +49,7 @@ struct FusedArgs {
 // steps s >= S are never contracted.  (A predicated load makes hipcc branch around it and wait vmcnt(0) right
 // after it, serialising the group.)  Wave-uniform 64-bit base per (step, q) plus one per-lane 32-bit offset
 // keeps the addresses in SGPRs.  Raw bytes are kept; the signed-sample flip happens at the consumer.
+template <bool Nt = false>
 __device__ __forceinline__ void load_group(const uint8_t* __restrict__ base, size_t ant_stride, int tq, int T4, int g,
                                            int A, int h, uint32_t (&d)[kGroup][4][4]) {
   const int tqc = tq < T4 ? tq : T4 - 1;
@@ -53,12 +59,13 @@ __device__ __forceinline__ void load_group(const uint8_t* __restrict__ base, siz
     for (int q = 0; q < 4; ++q) {
       int a = 16 * (g + ss) + 4 * h + q;
       a = a < A ? a : A - 1;
-      const uint4 v = *reinterpret_cast<const uint4*>(base + static_cast<size_t>(a) * ant_stride +
-                                                      static_cast<uint32_t>(tqc) * 16u);
-      d[ss][q][0] = v.x;
-      d[ss][q][1] = v.y;
-      d[ss][q][2] = v.z;
-      d[ss][q][3] = v.w;
+      const u32x4_t* src = reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a) * ant_stride +
+                                                            static_cast<uint32_t>(tqc) * 16u);
+      const u32x4_t v = Nt ? __builtin_nontemporal_load(src) : *src;
+      d[ss][q][0] = v[0];
+      d[ss][q][1] = v[1];
+      d[ss][q][2] = v[2];
+      d[ss][q][3] = v[3];
     }
   }
 }
@@ -198,7 +205,7 @@ __device__ __forceinline__ void contract_pol(const half8* __restrict__ buf, int 
 
 // Store one pol's beams of the 4 samples of quad tq.  Full: every tile complete and 16-byte aligned (2M a
 // multiple of 16*NTS), so each is one unconditional 16-byte (f32) / 4-byte (int8) store.
-template <bool OutI8, int NTS, bool Full>
+template <bool OutI8, int NTS, bool Full, bool Nt = false>
 __device__ __forceinline__ void store_pol(const FusedArgs& P, int b, int c, int p, int tau0, int nts, int tq, int h,
                                           const f32x4 (&acc)[4][NTS]) {
   const int M2 = 2 * P.M;
@@ -223,7 +230,11 @@ __device__ __forceinline__ void store_pol(const FusedArgs& P, int b, int c, int 
         } else {
           float* o = reinterpret_cast<float*>(P.y) + orow * M2;
           if constexpr (Full) {
-            *reinterpret_cast<f32x4*>(o + col0) = acc[i][tau];
+            if constexpr (Nt) {
+              __builtin_nontemporal_store(acc[i][tau], reinterpret_cast<f32x4*>(o + col0));
+            } else {
+              *reinterpret_cast<f32x4*>(o + col0) = acc[i][tau];
+            }
           } else {
             store_f32<NTS>(o, col0, M2, acc[i][tau]);
           }
@@ -343,8 +354,8 @@ __global__ __launch_bounds__(kThreads, 2) void beamform_fused_pipe_kernel(FusedA
 // Issue order delay model -> voltages (16 x 16 B per lane, all in flight) -> coefficient math under them ->
 // barrier -> per pol: MFMA contraction + stores.  Memory/compute overlap comes from the 3+ workgroups a CU holds
 // at this register footprint (the hardware interleaves their phases).
-template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
-__global__ __launch_bounds__(kThreads) void beamform_fused_item_kernel(FusedArgs P) {
+template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0, int Occ = 1>
+__global__ __launch_bounds__(kThreads, Occ) void beamform_fused_item_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
@@ -372,7 +383,7 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_item_kernel(FusedArgs
         for (int j = 0; j < 4; ++j) d[ss][q][j] = static_cast<uint32_t>(tid * 0x01010101u + ss + q + j);
   } else {
     const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
-    load_group(base, ant_stride, tq, T4, 0, P.A, h, d);
+    load_group<(Mode & kCachedLoad) == 0>(base, ant_stride, tq, T4, 0, P.A, h, d);
   }
   __builtin_amdgcn_sched_barrier(0);
   make_coefs<Exact, Mode, NTS>(reinterpret_cast<_Float16*>(lds), cp, P, b, c, tau0, nts, tid);
@@ -401,7 +412,7 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_item_kernel(FusedArgs
         for (int tau = 0; tau < NTS; ++tau) sum += acc[i][tau][0] + acc[i][tau][1] + acc[i][tau][2] + acc[i][tau][3];
       if (sum == 1234.5f) reinterpret_cast<float*>(P.y)[tid] = sum;
     } else {
-      if (tv) store_pol<OutI8, NTS, Full>(P, b, c, p, tau0, nts, tq, h, acc);
+      if (tv) store_pol<OutI8, NTS, Full, (Mode & kNtStore) != 0>(P, b, c, p, tau0, nts, tq, h, acc);
     }
   }
 }
@@ -496,13 +507,13 @@ int launch_pipe(FusedArgs P, hipStream_t st) {
   BF_LAUNCHED("beamform_fused_pipe_kernel");
 }
 
-template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
+template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0, int Occ = 1>
 int launch_item(FusedArgs P, hipStream_t st) {
   P.nslabs = (P.NT + NTS - 1) / NTS;
   const size_t lds = coef_lds_bytes(P.S, NTS);
   const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
   BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many (batch, channel) items");
-  hipLaunchKernelGGL((beamform_fused_item_kernel<Signed, OutI8, NTS, Exact, Full, Mode>),
+  hipLaunchKernelGGL((beamform_fused_item_kernel<Signed, OutI8, NTS, Exact, Full, Mode, Occ>),
                      dim3(static_cast<unsigned>(n_items)), dim3(kThreads), lds, st, P);
   BF_LAUNCHED("beamform_fused_item_kernel");
 }
@@ -600,9 +611,10 @@ extern "C" double bf_fused_algorithmic_bytes(int B, int C, int T, int A, int M, 
 
 #ifdef BF_DIAG
 namespace bf {
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Streams in_bytes in and out_bytes out with 16-byte lanes, `unroll` loads in flight per lane before the stores:
 // the achievable HBM ceiling for the fused kernel's traffic mix.
-template <int U>
+template <int U, bool NtLoad = false, bool NtStore = false>
 __global__ __launch_bounds__(256) void stream_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n_in,
                                                      size_t n_out) {
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
@@ -612,12 +624,27 @@ __global__ __launch_bounds__(256) void stream_kernel(const uint4* __restrict__ i
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t i = i0 + u * stride;
-      v[u] = (i < n_in) ? in[i] : make_uint4(static_cast<uint32_t>(i), 1, 2, 3);
+      if (i < n_in) {
+        if constexpr (NtLoad) {
+          const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + i));
+          v[u] = make_uint4(t[0], t[1], t[2], t[3]);
+        } else {
+          v[u] = in[i];
+        }
+      } else {
+        v[u] = make_uint4(static_cast<uint32_t>(i), 1, 2, 3);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t i = i0 + u * stride;
-      if (i < n_out) out[i] = v[u];
+      if (i < n_out) {
+        if constexpr (NtStore) {
+          __builtin_nontemporal_store(u32x4{v[u].x, v[u].y, v[u].z, v[u].w}, reinterpret_cast<u32x4*>(out + i));
+        } else {
+          out[i] = v[u];
+        }
+      }
     }
   }
 }
@@ -627,7 +654,16 @@ extern "C" int bf_diag_stream(const void* in, void* out, size_t in_bytes, size_t
                               void* stream) {
   auto in4 = reinterpret_cast<const uint4*>(in);
   auto out4 = reinterpret_cast<uint4*>(out);
-  if (unroll >= 8)
+  if (unroll == 101)
+    hipLaunchKernelGGL((bf::stream_kernel<1, false, true>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
+                       in_bytes / 16, out_bytes / 16);
+  else if (unroll == 102)
+    hipLaunchKernelGGL((bf::stream_kernel<1, true, false>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
+                       in_bytes / 16, out_bytes / 16);
+  else if (unroll == 103)
+    hipLaunchKernelGGL((bf::stream_kernel<1, true, true>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
+                       in_bytes / 16, out_bytes / 16);
+  else if (unroll >= 8)
     hipLaunchKernelGGL(bf::stream_kernel<8>, dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4, in_bytes / 16,
                        out_bytes / 16);
   else if (unroll >= 4)
@@ -674,6 +710,9 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 9: return bf::launch_item<true, false, 2, false, true, 9>(P, st);
       case 11: return bf::launch_item<true, false, 2, false, true, 11>(P, st);
       case 16: return bf::launch_item<true, false, 2, true, true, 0>(P, st);
+      case 128: return bf::launch_item<true, false, 2, false, true, 128>(P, st);
+      case 256: return bf::launch_item<true, false, 2, false, true, 256>(P, st);
+      case 384: return bf::launch_item<true, false, 2, false, true, 384>(P, st);
       default: bf::set_error("bad mode"); return BF_ERR_ARG;
     }
   }

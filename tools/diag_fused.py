@@ -3,6 +3,7 @@
 Modes: 1 skip coefficient generation, 2 skip MFMA (cheap VALU reduction instead), 4 skip stores,
 8 skip loads (synthetic registers).  Times are HIP-event averages over N launches, 2 rotating buffer sets."""
 import ctypes, os, sys
+import os as _os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np
@@ -36,17 +37,33 @@ def timeit(fn, n=20):
     return e1.time_since(e0) / n
 
 
-names = {0: "full (fast coef)", 16: "full (exact coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
+names = {0: "full (fast coef)", 128: "cached loads", 256: "nt stores", 384: "cached loads+nt st",
+         16: "full (exact coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
          3: "no-coef,no-mfma", 5: "no-coef,no-store", 9: "no-coef,no-load", 7: "loads only", 11: "stores only"}
 print(f"shape B={B} C={C} T={T} A={A} M={M}: in {nin/2**30:.2f} GiB out {nout/2**30:.2f} GiB")
+ROUNDS = int(_os.environ.get("DIAG_ROUNDS", "1"))
 for kbase, kname in ((0, "pipe"), (32, "item")):
-    for mode, name in names.items():
-        t = timeit(lambda i: lib.bf_diag_fused(kbase + mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr, B, C, T,
-                                               A, M, C, 1 / 1712e6, q.handle))
-        print(f"  {kname} mode {mode:2d} {name:18s} {t*1e6:9.1f} us   alg {alg/t/1e9:7.1f} GB/s")
-for grid in (1024, 2048, 8192):
-    for unroll in (1, 4, 8):
-        for (ri, wo, nm) in ((nin, nout, "read+write"), (nin, 0, "read only"), (0, nout, "write only")):
-            t = timeit(lambda i: lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, ri, wo, grid, unroll,
-                                                    q.handle))
-            print(f"  stream grid {grid:5d} unroll {unroll} {nm:11s} {t*1e6:8.1f} us  {(ri + wo)/t/1e9:7.1f} GB/s")
+    if _os.environ.get("DIAG_KERNELS", "item,pipe").find(kname) < 0:
+        continue
+    only = _os.environ.get("DIAG_MODES")
+    modes = [m for m in names if not (kname == "pipe" and m >= 64)]
+    if only:
+        modes = [m for m in modes if str(m) in only.split(",")]
+    res = {m: [] for m in modes}
+    for r in range(ROUNDS):  # interleaved rounds (one process, same data): A/B-safe
+        for mode in modes:
+            res[mode].append(timeit(lambda i: lib.bf_diag_fused(kbase + mode, bufs[i % 2][0].ptr, dv.ptr,
+                                                                bufs[i % 2][1].ptr, B, C, T, A, M, C, 1 / 1712e6,
+                                                                q.handle)))
+    for mode in modes:
+        ts = sorted(res[mode])
+        med, mn = ts[len(ts) // 2], ts[0]
+        print(f"  {kname} mode {mode:3d} {names[mode]:18s} median {med*1e6:8.1f} us  min {mn*1e6:8.1f} us  "
+              f"alg {alg/med/1e9:7.1f} GB/s  ({len(ts)} rounds)")
+if _os.environ.get("DIAG_STREAMS", "1") == "1":
+    for grid in (512, 1024, 2048):
+        for unroll, uname in ((1, "plain"), (101, "nt-store"), (102, "nt-load"), (103, "nt-both")):
+            for (ri, wo, nm) in ((nin, nout, "read+write"), (nin, 0, "read only"), (0, nout, "write only")):
+                t = timeit(lambda i: lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, ri, wo, grid, unroll,
+                                                        q.handle))
+                print(f"  stream grid {grid:5d} {uname:8s} {nm:11s} {t*1e6:8.1f} us  {(ri + wo)/t/1e9:7.1f} GB/s")
