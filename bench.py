@@ -215,6 +215,23 @@ def pmc_traffic(args):
     return traffic, vals
 
 
+KERNELS = {False: ("beamform_fused_item_kernel",
+                  "f16 hi/lo-split coefficients on v_mfma_f32_16x16x32_f16, f32 accumulation"),
+           True: ("beamform_fused_i8_item_kernel",
+                  "Q14 two-limb int8 coefficients on v_mfma_i32_16x16x64_i8, exact int32 accumulation, int8 beams")}
+
+
+def secondary(args, dist, workload, out_int8):
+    sub = argparse.Namespace(**{**vars(args), "workload": workload, "out_int8": out_int8})
+    r = run_gpu(sub, dist, WORKLOADS[workload])
+    r.pop("out")
+    return {"workload": workload + ": " + WORKLOADS[workload]["desc"], "output": "int8" if out_int8 else "float32",
+            "kernel": KERNELS[out_int8][0],
+            "value": round(r["samples_per_step"] * args.steps / r["t_max"] / 1e9, 2), "unit": "Gsamples/s",
+            "roofline_frac": round(r["alg_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
+            "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"]}
+
+
 def main():
     args = parse()
     wl = WORKLOADS[args.workload]
@@ -237,27 +254,22 @@ def main():
                    "n_pols": 2, "output": "int8" if args.out_int8 else "float32",
                    "parallelism": f"channel-shard x{dist.world} (xeng_id = rank), no data-path collective"},
         "beams_per_s": round(r["beams_per_step"] * args.steps * dist.world / r["t_max"], 1),
-        "compute": "f16 hi/lo-split coefficients on v_mfma_f32_16x16x32_f16, f32 accumulation",
+        "compute": KERNELS[args.out_int8][1],
         "device": r["device"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "beamform_fused_item_kernel", "avg_launch_us": round(r["kernel_s"] * 1e6, 2),
+                     "kernel": KERNELS[args.out_int8][0], "avg_launch_us": round(r["kernel_s"] * 1e6, 2),
                      "alg_bytes_per_launch": r["alg_bytes"]},
         "cpu_baseline": None,
     }
     del ops_queue
     if dist.rank == 0 and dist.world == 1 and not args.no_secondary and args.workload == "cfg3":
-        try:
-            sub = argparse.Namespace(**{**vars(args), "workload": "cfg2"})
-            r2 = run_gpu(sub, dist, WORKLOADS["cfg2"])
-            r2.pop("out")
-            line["secondary"] = {
-                "workload": "cfg2: " + WORKLOADS["cfg2"]["desc"],
-                "value": round(r2["samples_per_step"] * args.steps / r2["t_max"] / 1e9, 2), "unit": "Gsamples/s",
-                "roofline_frac": round(r2["alg_bytes"] / r2["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
-                "avg_launch_us": round(r2["kernel_s"] * 1e6, 2)}
-        except Exception as e:  # secondary line is informational
-            line["secondary"] = {"error": str(e)[:200]}
+        line["secondary"] = []
+        for workload, out_int8 in (("cfg2", args.out_int8), ("cfg3", not args.out_int8)):
+            try:
+                line["secondary"].append(secondary(args, dist, workload, out_int8))
+            except Exception as e:  # secondary lines are informational
+                line["secondary"].append({"workload": workload, "error": str(e)[:200]})
     if dist.rank == 0 and dist.world == 1 and not args.no_pmc:
         try:
             traffic, info = pmc_traffic(args)

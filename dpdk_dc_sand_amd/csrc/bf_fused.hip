@@ -170,14 +170,22 @@ __device__ __forceinline__ void gen_coefs(_Float16* lh, const FusedArgs& P, int 
 }
 
 // Contract one pol of one group: acc[i][tau] += W^T(s, tau) . X(s, sample 4tq+i, pol p).
-template <bool Signed, int NTS, bool Full>
+// FlipHere: flip the signed samples' sign bits of step s in place just before its first use (pol 0), so step 0's
+// MFMAs only wait for step 0's loads while the later steps are still in flight.
+template <bool Signed, int NTS, bool Full, bool FlipHere = false>
 __device__ __forceinline__ void contract_pol(const half8* __restrict__ buf, int g, int S, int nts, int lane, int p,
-                                             const uint32_t (&d)[kGroup][4][4], f32x4 (&acc)[4][NTS]) {
+                                             uint32_t (&d)[kGroup][4][4], f32x4 (&acc)[4][NTS]) {
   const uint32_t sel = p ? kSelHi : kSelLo;
 #pragma unroll
   for (int ss = 0; ss < kGroup; ++ss) {
     const int s = g + ss;
     if (s >= S) break;
+    if constexpr (Signed && FlipHere) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[ss][q][j] ^= 0x80808080u;
+    }
     half8 chi[NTS], clo[NTS];
 #pragma unroll
     for (int tau = 0; tau < NTS; ++tau) {
@@ -388,7 +396,6 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_item_kernel(Fuse
   __builtin_amdgcn_sched_barrier(0);
   make_coefs<Exact, Mode, NTS>(reinterpret_cast<_Float16*>(lds), cp, P, b, c, tau0, nts, tid);
   __syncthreads();
-  flip_group<Signed>(d);
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     f32x4 acc[4][NTS];
@@ -402,7 +409,11 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_item_kernel(Fuse
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][0][q] = __builtin_bit_cast(float, d[q][p + 1][i] ^ d[q][p][i]);
     } else {
-      contract_pol<Signed, NTS, Full>(lds, 0, P.S, nts, lane, p, d, acc);
+      if (p == 0) {
+        contract_pol<Signed, NTS, Full, true>(lds, 0, P.S, nts, lane, 0, d, acc);
+      } else {
+        contract_pol<Signed, NTS, Full, false>(lds, 0, P.S, nts, lane, 1, d, acc);
+      }
     }
     if constexpr (Mode & kSkipStore) {
       float sum = 0.f;
@@ -473,6 +484,391 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
       store_pol<OutI8, NTS, false>(P, b, c, 1, tau0, nts, tq, h, acc[1]);
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Integer int8-output kernel: bit-exact requantised beams.
+//
+// Contract (oracle.fused_beamform_int8): W = rne(w * 2^14) from the exact float32 phasor w (Q14, |W| <= 16384),
+// y = sum_k x_k W_k exactly (integers), q = clamp(rne(f32(y) * f32(scale * 2^-14)), -127, 127).  The float rounding
+// is single, deterministic and restated in NumPy, so the output matches the oracle bit for bit.
+// On v_mfma_i32_16x16x64_i8 (lane l: A[row l&15][kslot(l>>4, byte j)], B[kslot(l>>4, j)][col l&15], probed in
+// tools/probes/mfma_i8_layout.hip): W = 256 W_hi + W_lo in balanced int8 limbs, per 16x16 tile
+//     t = (sum hi * x) << 8;  t += sum lo * x        (i32, exact for A <= 256)
+// i.e. half the MFMAs of the f16 hi/lo path and no byte->f16 conversion: each fragment dword is one v_perm of
+// two antennas' raw dwords.  k-slot (s, h, j) <-> antenna a = 32 s + 8 h + j/2, re/im = j & 1.  Unsigned samples
+// run as x - 128 (one xor) plus the exact correction 128 * sum_k W_k per column.
+inline int fused_kernel_choice();
+constexpr uint32_t kSelP0 = 0x05040100u;  // v_perm: [S1.b0, S1.b1, S0.b0, S0.b1]
+constexpr uint32_t kSelP1 = 0x07060302u;  // v_perm: [S1.b2, S1.b3, S0.b2, S0.b3]
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4_t mfma_i8(i32x4_t a, i32x4_t b, i32x4_t c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+// LDS image: [s][tau][limb][lane] x 16 bytes, then 16*NTS int32 column sums.
+__device__ __forceinline__ int coef8_byte(int k, int cl, int nts, int limb) {
+  const int s = k >> 6, h = (k >> 4) & 3, j = k & 15, tau = cl >> 4, row = cl & 15;
+  return ((((s * nts + tau) * 2 + limb) * 64) + row + 16 * h) * 16 + j;
+}
+
+__device__ __forceinline__ void put_q14(int8_t* lb, int* colsum, int k, int cl, int nts, float w) {
+  const int W = static_cast<int>(__builtin_rintf(w * 16384.0f));  // exact product, RNE
+  const int lo = ((W + 128) & 255) - 128;
+  const int hi = (W - lo) >> 8;
+  lb[coef8_byte(k, cl, nts, 0)] = static_cast<int8_t>(hi);
+  lb[coef8_byte(k, cl, nts, 1)] = static_cast<int8_t>(lo);
+  if (W) atomicAdd(colsum + cl, W);
+}
+
+// grid = B*C*nslabs; any A (groups of 64 antennas = two i8 k-steps), any T (64-sample chunks per wave).
+template <bool Signed, int NTS>
+__global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P) {
+  extern __shared__ __attribute__((aligned(16))) half8 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const int slab = blockIdx.x % P.nslabs;
+  const int bc = blockIdx.x / P.nslabs;
+  const int b = bc / P.C, c = bc % P.C;
+  const int tau0 = slab * NTS;
+  const int nts = min(NTS, P.NT - tau0);
+  const int S8 = (2 * P.A + 63) / 64;  // i8 k-steps
+  const int T4 = P.T >> 2;
+  const int nchunks = (T4 + 15) >> 4;
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+  int8_t* lb = reinterpret_cast<int8_t*>(lds);
+  int* colsum = reinterpret_cast<int*>(lb + static_cast<size_t>(S8) * nts * 2 * 64 * 16);
+  const int M2 = 2 * P.M;
+
+  // 1. coefficients (exact float64 phasors) -> Q14 limbs + column sums
+  for (int e = tid; e < nts * 16; e += kThreads) colsum[e] = 0;
+  __syncthreads();
+  {
+    const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+    const int cd = P.delay_channels == 1 ? 0 : c;
+    const int nbeam = nts * 8;
+    const int npairs = S8 * 32 * nbeam;
+    const double ch = static_cast<double>(P.base_ch + c);
+    for (int e = tid; e < npairs; e += kThreads) {
+      const int a = e / nbeam, ml = e - a * nbeam;
+      const int m = tau0 * 8 + ml;
+      float re = 0.0f, im = 0.0f;
+      if (a < P.A && m < P.M)
+        steering_coeff(P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a], ch, P.ctot, P.ts, dt, &re, &im);
+      const int cl = 2 * ml;
+      put_q14(lb, colsum, 2 * a, cl, nts, re);
+      put_q14(lb, colsum, 2 * a, cl + 1, nts, im);
+      put_q14(lb, colsum, 2 * a + 1, cl, nts, -im);
+      put_q14(lb, colsum, 2 * a + 1, cl + 1, nts, re);
+    }
+  }
+  __syncthreads();
+  const int4* fr = reinterpret_cast<const int4*>(lds);
+  const float s32 = P.out_scale * 0x1p-14f;  // exact: power-of-two scaling
+
+  for (int chunk = wave; chunk < nchunks; chunk += kWaves) {
+    const int tq = chunk * 16 + tl;
+    const bool tv = tq < T4;
+    const int tqc = tv ? tq : T4 - 1;
+    i32x4_t acc[2][4][NTS];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau) acc[p][i][tau] = i32x4_t{0, 0, 0, 0};
+    for (int g = 0; g < S8; g += 2) {  // 64 antennas per group: 2 k-steps x 8 antennas per lane
+      uint32_t d[2][8][4];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          int a = 32 * (g + ss) + 8 * h + q;
+          a = a < P.A ? a : P.A - 1;  // padded antennas meet zero coefficients
+          const u32x4_t v = __builtin_nontemporal_load(
+              reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a) * ant_stride + tqc * 16u));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d[ss][q][j] = Signed ? v[j] : (v[j] ^ 0x80808080u);
+        }
+      }
+#pragma unroll
+      for (int tau = 0; tau < NTS; ++tau) {
+        if (tau >= nts) break;
+        i32x4_t chi[2], clo[2];
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const int s = min(g + ss, S8 - 1);
+          const int4 x0 = fr[(((s * nts + tau) * 2 + 0) * 64) + lane];
+          const int4 x1 = fr[(((s * nts + tau) * 2 + 1) * 64) + lane];
+          chi[ss] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
+          clo[ss] = (g + ss < S8) ? i32x4_t{x1.x, x1.y, x1.z, x1.w} : i32x4_t{0, 0, 0, 0};
+          if (g + ss >= S8) chi[ss] = i32x4_t{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const uint32_t sel = p ? kSelP1 : kSelP0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            i32x4_t f[2];
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss)
+              f[ss] = i32x4_t{static_cast<int>(__builtin_amdgcn_perm(d[ss][1][i], d[ss][0][i], sel)),
+                              static_cast<int>(__builtin_amdgcn_perm(d[ss][3][i], d[ss][2][i], sel)),
+                              static_cast<int>(__builtin_amdgcn_perm(d[ss][5][i], d[ss][4][i], sel)),
+                              static_cast<int>(__builtin_amdgcn_perm(d[ss][7][i], d[ss][6][i], sel))};
+            i32x4_t t = mfma_i8(chi[0], f[0], i32x4_t{0, 0, 0, 0});
+            t = mfma_i8(chi[1], f[1], t);
+            t = t << 8;
+            t = mfma_i8(clo[0], f[0], t);
+            t = mfma_i8(clo[1], f[1], t);
+            acc[p][i][tau] += t;
+          }
+        }
+      }
+    }
+    if (!tv) continue;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq + i;
+        int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow * M2;
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau) {
+          if (tau >= nts) break;
+          const int col0 = 16 * (tau0 + tau) + 4 * h;
+          uint32_t packed = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            int y = acc[p][i][tau][r];
+            if constexpr (!Signed) {
+            const int cl = 16 * tau + 4 * h + r;
+            y += 128 * (colsum[cl] + colsum[32 + cl] + colsum[64 + cl] + colsum[96 + cl]);
+          }  // x = (x - 128) + 128
+            float v = __builtin_rintf(static_cast<float>(y) * s32);
+            v = fminf(fmaxf(v, -127.0f), 127.0f);
+            packed |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(v)))) << (8 * r);
+          }
+          if ((M2 & 3) == 0 && col0 + 4 <= M2) {
+            *reinterpret_cast<uint32_t*>(o + col0) = packed;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (col0 + r < M2) o[col0 + r] = static_cast<int8_t>((packed >> (8 * r)) & 255);
+          }
+        }
+      }
+    }
+  }
+}
+
+// Item form of the integer kernel (A <= 64, T <= 256): one (slab, b, c) per workgroup, issue order delay model ->
+// voltages (16 x 16 B per lane) -> exact coefficients + Q14 limbs under them -> barrier -> per pol: v_perm
+// fragments, 8 i8 MFMAs per (sample, tile), requantise, 4-byte stores.
+template <bool Signed, int NTS, bool Full>
+__global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedArgs P) {
+  extern __shared__ __attribute__((aligned(16))) half8 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const int T4 = P.T >> 2;
+  const int tq = wave * 16 + tl;
+  const bool tv = tq < T4;
+  const int tqc = tv ? tq : T4 - 1;
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  const int item = blockIdx.x;
+  const int c = item % P.C;
+  const int b = (item / P.C) % P.B;
+  const int slab = item / (P.C * P.B);
+  const int tau0 = slab * NTS;
+  const int nts = Full ? NTS : min(NTS, P.NT - tau0);
+  const int S8 = (2 * P.A + 63) / 64;  // 1 or 2
+  const int M2 = 2 * P.M;
+  int8_t* lb = reinterpret_cast<int8_t*>(lds);
+  int* colsum = reinterpret_cast<int*>(lb + static_cast<size_t>(2) * NTS * 2 * 64 * 16);
+
+  // 1. delay model (oldest), 2. voltages, 3. coefficients under them
+  CoefPrefetch<NTS> cp;
+  load_delays<NTS>(cp, P, c, tau0, nts, tid);
+  __builtin_amdgcn_sched_barrier(0);
+  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+  uint32_t d[2][8][4];
+#pragma unroll
+  for (int ss = 0; ss < 2; ++ss) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      int a = 32 * ss + 8 * h + q;
+      a = a < P.A ? a : P.A - 1;
+      const u32x4_t v = __builtin_nontemporal_load(
+          reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a) * ant_stride + tqc * 16u));
+      d[ss][q][0] = v[0];
+      d[ss][q][1] = v[1];
+      d[ss][q][2] = v[2];
+      d[ss][q][3] = v[3];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+    const int nbeam = nts * 8;
+    const int npairs = S8 * 32 * nbeam;
+    const double ch = static_cast<double>(P.base_ch + c);
+    // this thread's contributions to columns 2ml, 2ml+1: ml = tid % nbeam for every pair it owns (256 % nbeam == 0)
+    int cs0 = 0, cs1 = 0;
+#pragma unroll
+    for (int j = 0; j < CoefPrefetch<NTS>::kMaxPairs; ++j) {
+      const int e = tid + j * kThreads;
+      if (e >= npairs) break;
+      const int a = e / nbeam, ml = e - a * nbeam;
+      const int m = tau0 * 8 + ml;
+      float re = 0.0f, im = 0.0f;
+      if (a < P.A && m < P.M) steering_coeff(cp.dv[j], ch, P.ctot, P.ts, dt, &re, &im);
+      const int cl = 2 * ml;
+      const int Wc = static_cast<int>(__builtin_rintf(re * 16384.0f));
+      const int Ws = static_cast<int>(__builtin_rintf(im * 16384.0f));
+      const int ks[4] = {2 * a, 2 * a, 2 * a + 1, 2 * a + 1};
+      const int cs[4] = {cl, cl + 1, cl, cl + 1};
+      const int ws[4] = {Wc, Ws, -Ws, Wc};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lo = ((ws[r] + 128) & 255) - 128;
+        const int hi = (ws[r] - lo) >> 8;
+        lb[coef8_byte(ks[r], cs[r], nts, 0)] = static_cast<int8_t>(hi);
+        lb[coef8_byte(ks[r], cs[r], nts, 1)] = static_cast<int8_t>(lo);
+      }
+      cs0 += Wc - Ws;  // column 2m:   W[2a][2m] + W[2a+1][2m]
+      cs1 += Ws + Wc;  // column 2m+1: W[2a][2m+1] + W[2a+1][2m+1]
+    }
+    if constexpr (!Signed) {
+      // nbeam (8 or 16) divides 64: lanes with equal lane % nbeam share ml; reduce them, one partial per wave
+      for (int off = nbeam; off < 64; off <<= 1) {
+        cs0 += __shfl_xor(cs0, off);
+        cs1 += __shfl_xor(cs1, off);
+      }
+      if (lane < nbeam) {
+        colsum[wave * 32 + 2 * lane] = cs0;
+        colsum[wave * 32 + 2 * lane + 1] = cs1;
+      }
+    }
+  }
+  __syncthreads();
+  const int4* fr = reinterpret_cast<const int4*>(lds);
+  const float s32 = P.out_scale * 0x1p-14f;
+
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const uint32_t sel = p ? kSelP1 : kSelP0;
+    i32x4_t acc[4][NTS];
+#pragma unroll
+    for (int tau = 0; tau < NTS; ++tau) {
+      if (!Full && tau >= nts) break;
+      i32x4_t chi[2], clo[2];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        if (ss < S8) {
+          const int4 x0 = fr[(((ss * nts + tau) * 2 + 0) * 64) + lane];
+          const int4 x1 = fr[(((ss * nts + tau) * 2 + 1) * 64) + lane];
+          chi[ss] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
+          clo[ss] = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+        } else {
+          chi[ss] = clo[ss] = i32x4_t{0, 0, 0, 0};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        i32x4_t f[2];
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          uint32_t w[4];
+#pragma unroll
+          for (int m2 = 0; m2 < 4; ++m2) {
+            uint32_t lo = d[ss][2 * m2][i], hi = d[ss][2 * m2 + 1][i];
+            if constexpr (!Signed) {
+              lo ^= 0x80808080u;
+              hi ^= 0x80808080u;
+            }
+            w[m2] = __builtin_amdgcn_perm(hi, lo, sel);
+          }
+          f[ss] = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]),
+                          static_cast<int>(w[3])};
+        }
+        i32x4_t t = mfma_i8(chi[0], f[0], i32x4_t{0, 0, 0, 0});
+        t = mfma_i8(chi[1], f[1], t);
+        t = t << 8;
+        t = mfma_i8(clo[0], f[0], t);
+        acc[i][tau] = mfma_i8(clo[1], f[1], t);
+      }
+    }
+    if (!tv) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq + i;
+      int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow * M2;
+#pragma unroll
+      for (int tau = 0; tau < NTS; ++tau) {
+        if (!Full && tau >= nts) break;
+        const int col0 = 16 * (tau0 + tau) + 4 * h;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int y = acc[i][tau][r];
+          if constexpr (!Signed) y += 128 * colsum[16 * tau + 4 * h + r];
+          float v = __builtin_rintf(static_cast<float>(y) * s32);
+          v = fminf(fmaxf(v, -127.0f), 127.0f);
+          packed |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(v)))) << (8 * r);
+        }
+        if (Full || ((M2 & 3) == 0 && col0 + 4 <= M2)) {
+          *reinterpret_cast<uint32_t*>(o + col0) = packed;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (col0 + r < M2) o[col0 + r] = static_cast<int8_t>((packed >> (8 * r)) & 255);
+        }
+      }
+    }
+  }
+}
+
+template <bool Signed, int NTS, bool Full>
+int launch_i8_item(FusedArgs P, hipStream_t st) {
+  P.nslabs = (P.NT + NTS - 1) / NTS;
+  const size_t lds = static_cast<size_t>(2) * NTS * 2 * 64 * 16 + 4 * 32 * 4;
+  const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
+  BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many items");
+  hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full>), dim3(static_cast<unsigned>(n_items)),
+                     dim3(kThreads), lds, st, P);
+  BF_LAUNCHED("beamform_fused_i8_item_kernel");
+}
+
+template <bool Signed>
+int launch_i8(FusedArgs P, hipStream_t st) {
+  const int S8 = (2 * P.A + 63) / 64;
+  if (S8 <= 2 && P.T <= 256 && fused_kernel_choice() != 2) {
+    const int M2 = 2 * P.M;
+    if (P.NT >= 2) {
+      if (M2 % 32 == 0) return launch_i8_item<Signed, 2, true>(P, st);
+      return launch_i8_item<Signed, 2, false>(P, st);
+    }
+    if (M2 == 16) return launch_i8_item<Signed, 1, true>(P, st);
+    return launch_i8_item<Signed, 1, false>(P, st);
+  }
+  auto lds_bytes = [&](int nts) { return static_cast<size_t>(S8) * nts * 2 * 64 * 16 + nts * 16 * 4; };
+  if (P.NT >= 2 && lds_bytes(2) <= kMaxLds) {
+    P.nslabs = (P.NT + 1) / 2;
+    const long long grid = static_cast<long long>(P.B) * P.C * P.nslabs;
+    BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
+    hipLaunchKernelGGL((beamform_fused_i8_kernel<Signed, 2>), dim3(static_cast<unsigned>(grid)), dim3(kThreads),
+                       lds_bytes(2), st, P);
+  } else {
+    BF_REQUIRE(lds_bytes(1) <= kMaxLds, "bf_beamform_fused: n_ants=%d too large", P.A);
+    P.nslabs = P.NT;
+    const long long grid = static_cast<long long>(P.B) * P.C * P.nslabs;
+    BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
+    hipLaunchKernelGGL((beamform_fused_i8_kernel<Signed, 1>), dim3(static_cast<unsigned>(grid)), dim3(kThreads),
+                       lds_bytes(1), st, P);
+  }
+  BF_LAUNCHED("beamform_fused_i8_kernel");
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -592,6 +988,10 @@ extern "C" int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, in
   P.out_scale = out_scale;
   hipStream_t st = bf::as_stream(stream);
   const bool sgn = flags & BF_FUSED_SIGNED, i8 = flags & BF_FUSED_OUT_INT8, ex = flags & BF_FUSED_EXACT_COEFF;
+  if (i8) {
+    const char* e = getenv("BF_FUSED_INT8_FLOAT");  // measurement: float path + requantise instead
+    if (!(e && e[0] == '1')) return sgn ? bf::launch_i8<true>(P, st) : bf::launch_i8<false>(P, st);
+  }
   if (sgn) {
     if (i8) return ex ? bf::dispatch<true, true, true>(P, st) : bf::dispatch<true, true, false>(P, st);
     return ex ? bf::dispatch<true, false, true>(P, st) : bf::dispatch<true, false, false>(P, st);

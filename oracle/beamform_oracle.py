@@ -154,3 +154,28 @@ def requantise(y, scale):
     y * scale, saturated to [-127, 127] (symmetric, so conjugation never overflows).  int8 output."""
     v = np.rint(np.asarray(y, np.float32) * np.float32(scale))
     return np.clip(v, -127, 127).astype(np.int8)
+
+
+Q14 = 14  # fractional bits of the integer beamformer's coefficients
+
+
+def quantise_coeffs(w):
+    """Q14 steering coefficients: W = rne(w * 2^14) of the float32 coefficient (exact product), int64."""
+    return np.rint(np.asarray(w, np.float32).astype(np.float64) * (1 << Q14)).astype(np.int64)
+
+
+def fused_beamform_int8(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, scale=1.0,
+                        signed=False):
+    """Contract of the fused operator's int8 (requantised) output -- bit-exact:
+        W = rne(w * 2^14)  (w: the exact float32 coefficients of fused_tables, i.e. CoeffGenerator's at dt = 0)
+        y = sum_k x_k W_k  (exact integers)
+        q = clamp(rne(float32(y) * float32(float32(scale) * 2^-14)), -127, 127)
+    raw: (B, A, C, T, 2, 2) 8-bit -> int8 (B, 2, C, T/16, 16, 2M)."""
+    B, A, C, T, P, Z = raw.shape
+    W = quantise_coeffs(fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt))
+    xr = reorder(raw)
+    X = (xr.view(np.int8) if signed else xr).astype(np.int64).reshape(B, 2, C, T, 2 * A)
+    Y = np.matmul(X, W)
+    s = np.float32(np.float32(scale) * np.float32(2.0 ** -Q14))
+    q = np.rint(Y.astype(np.float32) * s)
+    return np.clip(q, -127, 127).astype(np.int8).reshape(B, 2, C, T // 16, 16, -1)

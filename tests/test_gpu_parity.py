@@ -284,7 +284,35 @@ def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C
     assert_beams_allclose(y, ref, O.reorder(raw), w, signed=signed)
 
 
-def test_fused_int8_output_is_requantised_f32(context, command_queue, fused_path):
+@pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
+    (64, 16, 4, 256, 2, 1, True), (64, 16, 3, 256, 2, 3, False), (64, 1, 5, 256, 2, 1, True),
+    (19, 3, 7, 48, 2, 7, False), (130, 9, 2, 64, 2, 1, True), (256, 64, 1, 32, 1, 1, False),
+    (4, 1, 16, 1024, 1, 16, True), (80, 24, 3, 16, 3, 1, True), (32, 8, 4, 64, 2, 1, False),
+    (48, 12, 2, 128, 2, 1, False), (33, 5, 3, 80, 2, 3, True)])
+@pytest.mark.parametrize("i8_kernel", ["item", "generic"])
+def test_fused_int8_bit_exact(context, command_queue, monkeypatch, i8_kernel, A, M, C, T, B, dch, signed):
+    """int8 (requantised) beams: the integer MFMA path reproduces the oracle's integer contract bit for bit, on the
+    item kernel (A <= 64, T <= 256; others fall through to generic) and the generic kernel (any A, T)."""
+    monkeypatch.setenv("BF_FUSED_KERNEL", i8_kernel)
+    Ctot, xeng, t0, bdt = 4096, 1, 1e-3, 256 * 8192 * TS
+    d = random_delays(dch, M, A, A * 7 + M)
+    rng = np.random.default_rng(A * 3 + C)
+    raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8)
+    if signed:
+        raw = raw.view(np.int8)
+    for scale in (1.0 / 64, 1.0 / 16):
+        op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=dch, sample_signed=signed,
+                                     out_int8=True, out_scale=scale, t0=t0, batch_dt=bdt).instantiate(command_queue)
+        (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+        ref = O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, scale=scale, signed=signed)
+        assert q.dtype == np.int8
+        np.testing.assert_array_equal(q, ref)
+        assert np.abs(ref.astype(int)).max() >= 4  # not a trivially zero case
+
+
+def test_fused_int8_float_path_is_requantised_f32(context, command_queue, monkeypatch):
+    """Measurement path (BF_FUSED_INT8_FLOAT=1): float beams requantised in-kernel == bf_requant(float beams)."""
+    monkeypatch.setenv("BF_FUSED_INT8_FLOAT", "1")
     B, A, M, C, T, Ctot = 2, 64, 16, 4, 256, 4096
     d = random_delays(1, M, A, 9)
     raw = O.u8_voltages((B, A, C, T, 2, 2), seed=9).view(np.int8)

@@ -84,3 +84,18 @@ def test_reference_tolerance_is_not_fp32_attainable():
     exact = np.matmul(x.reshape(B, 2, C, 256, 2 * A).astype(np.float64), w.astype(np.float64)).reshape(y32.shape)
     assert (np.abs(y32 - exact) > 1e-4 + 1e-4 * np.abs(exact)).sum() > 0
     assert_beams_allclose(y32, exact, x, w)
+
+
+def test_int8_contract_is_close_to_float_beams():
+    """The integer int8 contract (Q14 coefficients, exact integer sums) stays within one LSB of requantising the
+    float32 beams except at rounding ties."""
+    B, A, M, C, T, Ctot = 1, 19, 3, 5, 32, 1024
+    rng = np.random.default_rng(2)
+    d = np.zeros((C, M, A, 4), np.float32)
+    d[..., 0] = rng.uniform(0, 10 * O.TS_MEERKAT, (C, M, A))
+    d[..., 2] = rng.uniform(-np.pi, np.pi, (C, M, A))
+    raw = O.u8_voltages((B, A, C, T, 2, 2), seed=4)
+    q = O.fused_beamform_int8(raw, d, Ctot, scale=1 / 16).astype(int)
+    qf = O.requantise(O.fused_beamform(raw, d, Ctot), 1 / 16).astype(int)
+    assert np.abs(q - qf).max() <= 1
+    assert (q == qf).mean() > 0.99
