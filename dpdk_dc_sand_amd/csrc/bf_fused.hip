@@ -17,6 +17,7 @@
 //
 // Lane (tl = l&15, h = l>>4) owns time quad tq = 16*chunk + tl (samples 4tq .. 4tq+3) and, in k-step s,
 // antennas 16s + 4h + q (q = 0..3); 16 lanes cover 256 contiguous bytes of an antenna run.
+#include <algorithm>
 #include <cstdlib>
 
 #include "bf_mfma.hpp"
@@ -643,10 +644,7 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             int y = acc[p][i][tau][r];
-            if constexpr (!Signed) {
-            const int cl = 16 * tau + 4 * h + r;
-            y += 128 * (colsum[cl] + colsum[32 + cl] + colsum[64 + cl] + colsum[96 + cl]);
-          }  // x = (x - 128) + 128
+            if constexpr (!Signed) y += 128 * colsum[16 * tau + 4 * h + r];  // x = (x - 128) + 128
             float v = __builtin_rintf(static_cast<float>(y) * s32);
             v = fminf(fmaxf(v, -127.0f), 127.0f);
             packed |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(v)))) << (8 * r);
@@ -664,10 +662,44 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P
   }
 }
 
+// Requantise 4 int32 beam components (columns cl0..cl0+3 of the slab) to packed int8: the integer contract
+// q = clamp(rne(f32(y) * f32(scale * 2^-14)), +-127); unsigned input adds back 128 * column sum (4 wave partials).
+template <bool Signed>
+__device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* colsum, int cl0, float s32) {
+  uint32_t packed = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    int y = acc[r];
+    if constexpr (!Signed) {  // x = (x - 128) + 128
+      const int cl = cl0 + r;
+      y += 128 * (colsum[cl] + colsum[32 + cl] + colsum[64 + cl] + colsum[96 + cl]);
+    }
+    float v = __builtin_rintf(static_cast<float>(y) * s32);
+    v = fminf(fmaxf(v, -127.0f), 127.0f);
+    packed |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(v)))) << (8 * r);
+  }
+  return packed;
+}
+
+// 4x4 transpose over (lane group h = lane >> 4, register i): afterwards lane group h holds v[i] = old v[h] of lane
+// group i.  Two stages of 2x2 block swaps (rows {0,1}<->{2,3}, then odd<->even rows); all 64 lanes must be active.
+__device__ __forceinline__ void transpose_rows4(uint32_t (&v)[4]) {
+  auto a = __builtin_amdgcn_permlane32_swap(v[0], v[2], false, false);
+  auto b = __builtin_amdgcn_permlane32_swap(v[1], v[3], false, false);
+  auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+  auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+  v[0] = c[0];
+  v[1] = c[1];
+  v[2] = d[0];
+  v[3] = d[1];
+}
+
 // Item form of the integer kernel (A <= 64, T <= 256): one (slab, b, c) per workgroup, issue order delay model ->
 // voltages (16 x 16 B per lane) -> exact coefficients + Q14 limbs under them -> barrier -> per pol: v_perm
 // fragments, 8 i8 MFMAs per (sample, tile), requantise, 4-byte stores.
-template <bool Signed, int NTS, bool Full>
+// Mode (diagnostics only): kSkipCoef / kSkipMfma / kSkipStore / kSkipLoad as the float item kernel; 16 = fast
+// (f32 sincos) coefficients instead of exact.
+template <bool Signed, int NTS, bool Full, int Mode = 0>
 __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -690,12 +722,19 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
 
   // 1. delay model (oldest), 2. voltages, 3. coefficients under them
   CoefPrefetch<NTS> cp;
-  load_delays<NTS>(cp, P, c, tau0, nts, tid);
+  if constexpr (!(Mode & kSkipCoef)) load_delays<NTS>(cp, P, c, tau0, nts, tid);
   __builtin_amdgcn_sched_barrier(0);
   const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
   uint32_t d[2][8][4];
 #pragma unroll
   for (int ss = 0; ss < 2; ++ss) {
+    if constexpr (Mode & kSkipLoad) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) d[ss][q][jj] = static_cast<uint32_t>(tid * 0x01010101u + ss + q + jj);
+      continue;
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       int a = 32 * ss + 8 * h + q;
@@ -723,7 +762,16 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
       const int a = e / nbeam, ml = e - a * nbeam;
       const int m = tau0 * 8 + ml;
       float re = 0.0f, im = 0.0f;
-      if (a < P.A && m < P.M) steering_coeff(cp.dv[j], ch, P.ctot, P.ts, dt, &re, &im);
+      if constexpr (Mode & kSkipCoef) {
+        re = 0.5f + 1e-3f * a;
+        im = 0.25f - 1e-3f * m;
+      } else if (a < P.A && m < P.M) {
+        if constexpr (Mode & 16) {
+          steering_coeff_fast(cp.dv[j], ch - P.ctot / 2.0, P.k, dt, &re, &im);
+        } else {
+          steering_coeff(cp.dv[j], ch, P.ctot, P.ts, dt, &re, &im);
+        }
+      }
       const int cl = 2 * ml;
       const int Wc = static_cast<int>(__builtin_rintf(re * 16384.0f));
       const int Ws = static_cast<int>(__builtin_rintf(im * 16384.0f));
@@ -777,6 +825,16 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        if constexpr (Mode & kSkipMfma) {
+          uint32_t x = static_cast<uint32_t>(chi[0][i] ^ clo[1][i]) + p;
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x = (x ^ d[ss][q][i]) + q;  // every load stays live
+          acc[i][tau] = i32x4_t{static_cast<int>(x), static_cast<int>(x >> 3), static_cast<int>(x >> 5),
+                                static_cast<int>(x >> 7)};
+          continue;
+        }
         i32x4_t f[2];
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
@@ -800,7 +858,69 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
         acc[i][tau] = mfma_i8(clo[1], f[1], t);
       }
     }
+    if constexpr (Full && !(Mode & kSkipStore)) {
+      // requantise, then a 4x4 transpose across the lane groups h (v_permlane32/16_swap) so lane (tl, h) holds
+      // all 16 * NTS bytes of output row 4 tq + h: a wave's 64 rows x 32 B go out as 2 KB of 16-B stores.
+      uint32_t pk[NTS][4];
+#pragma unroll
+      for (int tau = 0; tau < NTS; ++tau) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pk[tau][i] = requant4<Signed>(acc[i][tau], colsum, 16 * tau + 4 * h, s32);
+        transpose_rows4(pk[tau]);
+      }
+      if constexpr (Mode & 32) {  // diagnostics: contiguous 1 KB per store instruction (timing only, wrong data)
+        const size_t orow0 = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 64 * wave;
+        int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow0 * M2 + 16 * lane;
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau)
+          __builtin_nontemporal_store(u32x4_t{pk[tau][0], pk[tau][1], pk[tau][2], pk[tau][3]},
+                                      reinterpret_cast<u32x4_t*>(o + 1024 * tau));
+        continue;
+      }
+      if (M2 == 16 * NTS) {
+        // the slab is the whole row, so the wave's 64 rows are one contiguous 1-2 KB block: ds_bpermute the
+        // row-per-lane chunks so that store instruction s writes bytes [1024 s, 1024 s + 1024) of it.
+        const size_t orow0 = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 64 * wave;
+        int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow0 * M2 + 16 * lane;
+#pragma unroll
+        for (int si = 0; si < NTS; ++si) {
+          const int f = 64 * si + lane;  // flat 16-B chunk of the block
+          const int r = f / NTS, ch = f % NTS;
+          const int src = 4 * ((r >> 2) + 16 * (r & 3));  // lane (tl, h) = (r >> 2, r & 3) holds row r
+          uint32_t w[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            w[j] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(pk[0][j])));
+            if constexpr (NTS == 2) {
+              const uint32_t w1 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(pk[1][j])));
+              w[j] = ch ? w1 : w[j];
+            }
+          }
+          if (64 * wave + r < P.T)
+            __builtin_nontemporal_store(u32x4_t{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4_t*>(o + 1024 * si));
+        }
+        continue;
+      }
+      if (tv) {
+        const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq + h;
+        int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow * M2 + 16 * tau0;
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau)
+          __builtin_nontemporal_store(u32x4_t{pk[tau][0], pk[tau][1], pk[tau][2], pk[tau][3]},
+                                      reinterpret_cast<u32x4_t*>(o + 16 * tau));
+      }
+      continue;
+    }
     if (!tv) continue;
+    if constexpr (Mode & kSkipStore) {
+      int sum = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau) sum += acc[i][tau][0] ^ acc[i][tau][1] ^ acc[i][tau][2] ^ acc[i][tau][3];
+      if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[tid] = sum;
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq + i;
@@ -809,16 +929,8 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
       for (int tau = 0; tau < NTS; ++tau) {
         if (!Full && tau >= nts) break;
         const int col0 = 16 * (tau0 + tau) + 4 * h;
-        uint32_t packed = 0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int y = acc[i][tau][r];
-          if constexpr (!Signed) y += 128 * colsum[16 * tau + 4 * h + r];
-          float v = __builtin_rintf(static_cast<float>(y) * s32);
-          v = fminf(fmaxf(v, -127.0f), 127.0f);
-          packed |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(v)))) << (8 * r);
-        }
-        if (Full || ((M2 & 3) == 0 && col0 + 4 <= M2)) {
+        const uint32_t packed = requant4<Signed>(acc[i][tau], colsum, 16 * tau + 4 * h, s32);
+        if ((M2 & 3) == 0 && col0 + 4 <= M2) {
           *reinterpret_cast<uint32_t*>(o + col0) = packed;
         } else {
 #pragma unroll
@@ -830,13 +942,13 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
   }
 }
 
-template <bool Signed, int NTS, bool Full>
-int launch_i8_item(FusedArgs P, hipStream_t st) {
+template <bool Signed, int NTS, bool Full, int Mode = 0>
+int launch_i8_item(FusedArgs P, hipStream_t st, size_t min_lds = 0) {
   P.nslabs = (P.NT + NTS - 1) / NTS;
-  const size_t lds = static_cast<size_t>(2) * NTS * 2 * 64 * 16 + 4 * 32 * 4;
+  const size_t lds = std::max<size_t>(static_cast<size_t>(2) * NTS * 2 * 64 * 16 + 4 * 32 * 4, min_lds);
   const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
   BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many items");
-  hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full>), dim3(static_cast<unsigned>(n_items)),
+  hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode>), dim3(static_cast<unsigned>(n_items)),
                      dim3(kThreads), lds, st, P);
   BF_LAUNCHED("beamform_fused_i8_item_kernel");
 }
@@ -1097,6 +1209,24 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
   P.out_scale = 1.0f;
   hipStream_t st = bf::as_stream(stream);
   BF_REQUIRE(P.S <= bf::kGroup && T <= 256 && (2 * M) % 32 == 0, "diag: pipelined full-tile shapes only");
+  if (mode >= 512) {  // integer (int8-output) item kernel
+    P.out_scale = 1.0f / 64;
+    switch (mode - 512) {
+      case 0: return bf::launch_i8_item<true, 2, true, 0>(P, st);
+      case 1: return bf::launch_i8_item<true, 2, true, 1>(P, st);
+      case 2: return bf::launch_i8_item<true, 2, true, 2>(P, st);
+      case 3: return bf::launch_i8_item<true, 2, true, 3>(P, st);
+      case 4: return bf::launch_i8_item<true, 2, true, 4>(P, st);
+      case 5: return bf::launch_i8_item<true, 2, true, 5>(P, st);
+      case 7: return bf::launch_i8_item<true, 2, true, 7>(P, st);
+      case 8: return bf::launch_i8_item<true, 2, true, 8>(P, st);
+      case 16: return bf::launch_i8_item<true, 2, true, 16>(P, st);
+      case 32: return bf::launch_i8_item<true, 2, true, 32>(P, st);
+      case 64: return bf::launch_i8_item<true, 2, true, 0>(P, st, 60 * 1024);  // occupancy 2 (LDS-limited)
+      case 65: return bf::launch_i8_item<true, 2, true, 4>(P, st, 60 * 1024);
+      default: bf::set_error("bad mode"); return BF_ERR_ARG;
+    }
+  }
   if (mode >= 32) {
     switch (mode - 32) {
       case 0: return bf::launch_item<true, false, 2, false, true, 0>(P, st);

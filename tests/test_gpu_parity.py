@@ -288,7 +288,8 @@ def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C
     (64, 16, 4, 256, 2, 1, True), (64, 16, 3, 256, 2, 3, False), (64, 1, 5, 256, 2, 1, True),
     (19, 3, 7, 48, 2, 7, False), (130, 9, 2, 64, 2, 1, True), (256, 64, 1, 32, 1, 1, False),
     (4, 1, 16, 1024, 1, 16, True), (80, 24, 3, 16, 3, 1, True), (32, 8, 4, 64, 2, 1, False),
-    (48, 12, 2, 128, 2, 1, False), (33, 5, 3, 80, 2, 3, True)])
+    (48, 12, 2, 128, 2, 1, False), (33, 5, 3, 80, 2, 3, True), (16, 8, 3, 48, 2, 1, True),
+    (64, 16, 2, 112, 1, 1, False), (40, 32, 2, 64, 1, 2, True)])
 @pytest.mark.parametrize("i8_kernel", ["item", "generic"])
 def test_fused_int8_bit_exact(context, command_queue, monkeypatch, i8_kernel, A, M, C, T, B, dch, signed):
     """int8 (requantised) beams: the integer MFMA path reproduces the oracle's integer contract bit for bit, on the

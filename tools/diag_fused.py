@@ -42,11 +42,15 @@ names = {0: "full (fast coef)", 128: "cached loads", 256: "nt stores", 384: "cac
          3: "no-coef,no-mfma", 5: "no-coef,no-store", 9: "no-coef,no-load", 7: "loads only", 11: "stores only"}
 print(f"shape B={B} C={C} T={T} A={A} M={M}: in {nin/2**30:.2f} GiB out {nout/2**30:.2f} GiB")
 ROUNDS = int(_os.environ.get("DIAG_ROUNDS", "1"))
-for kbase, kname in ((0, "pipe"), (32, "item")):
-    if _os.environ.get("DIAG_KERNELS", "item,pipe").find(kname) < 0:
+names_i8 = {0: "full (exact coef)", 16: "fast coef", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store",
+            5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
+            65: "occ 2, no-store"}
+alg_i8 = nin + nout // 4
+for kbase, kname in ((0, "pipe"), (32, "item"), (512, "i8")):
+    if _os.environ.get("DIAG_KERNELS", "item,pipe,i8").find(kname) < 0:
         continue
     only = _os.environ.get("DIAG_MODES")
-    modes = [m for m in names if not (kname == "pipe" and m >= 64)]
+    modes = [m for m in (names_i8 if kname == "i8" else names) if not (kname == "pipe" and m >= 64)]
     if only:
         modes = [m for m in modes if str(m) in only.split(",")]
     res = {m: [] for m in modes}
@@ -58,8 +62,9 @@ for kbase, kname in ((0, "pipe"), (32, "item")):
     for mode in modes:
         ts = sorted(res[mode])
         med, mn = ts[len(ts) // 2], ts[0]
-        print(f"  {kname} mode {mode:3d} {names[mode]:18s} median {med*1e6:8.1f} us  min {mn*1e6:8.1f} us  "
-              f"alg {alg/med/1e9:7.1f} GB/s  ({len(ts)} rounds)")
+        nm, ab = (names_i8[mode], alg_i8) if kname == "i8" else (names[mode], alg)
+        print(f"  {kname} mode {mode:3d} {nm:18s} median {med*1e6:8.1f} us  min {mn*1e6:8.1f} us  "
+              f"alg {ab/med/1e9:7.1f} GB/s  ({len(ts)} rounds)")
 if _os.environ.get("DIAG_STREAMS", "1") == "1":
     for grid in (512, 1024, 2048):
         for unroll, uname in ((1, "plain"), (101, "nt-store"), (102, "nt-load"), (103, "nt-both")):
