@@ -51,6 +51,9 @@ PROTOTYPES = {
                             c_void_p]),
     "bf_beamform_fused": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                   c_int, c_double, c_double, c_double, c_int, c_float, c_void_p]),
+    "bf_beamform_fused_weighted": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                           c_int, c_int, c_int, c_double, c_double, c_double, c_int, c_float,
+                                           c_void_p]),
     "bf_requant": (c_int, [c_void_p, c_void_p, c_size_t, c_float, c_void_p]),
     "bf_fused_algorithmic_bytes": (c_double, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
 }

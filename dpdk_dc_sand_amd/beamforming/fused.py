@@ -8,6 +8,11 @@ cube once, generates each (b, c)'s coefficients in-kernel from the delay model (
 arithmetic as CoeffGenerator, so with zero rates the output equals OpSequence's), and writes the beams once:
 the HBM traffic is the algorithmic minimum.
 
+Beam weights (control-plane hook): the `?beam-weights <beam> w_0 .. w_{A-1}` request the
+control servlet forwards to the B-engines (ngkcs/ngkcs/corr3_servlet.py:140-153) sets one real weight per input
+for one beam.  With `beam_weights=True` the operator carries an (M, A) weight table (all ones initially) that is
+folded into the phasors in-kernel: W(a, m) = g(m, a) * (cos, sin) -- no extra pass, no extra HBM traffic.
+
 Per-block regeneration (BeamformerParameters.h:17 ACCUMULATIONS_BEFORE_NEW_COEFFS, the C++ study's
 time-dependent kernels BeamformerKernels.cu:121-189 and the fused study kernel :192-367): batch b is steered
 at dt_b = t0 + b * batch_dt using the delay and phase rates (SURVEY A3 convention).
@@ -31,13 +36,14 @@ class FusedBeamformerTemplate:
     t0, batch_dt: steering time of batch 0 and the step between batches (seconds).
     exact_coeffs: float64 phasors bit-exact to CoeffGenerator (then, with zero rates, the output equals
         OpSequence's bit for bit); default False = float32 phasors within ~1 ulp, several times cheaper.
+    beam_weights: carry a per-(beam, input) real weight table (slot beamWeights, set with set_beam_weights).
     """
 
     def __init__(self, context, n_batches: int, n_channels_per_stream: int, n_channels: int,
                  n_samples_per_channel: int, n_ants: int, n_beams: int, xeng_id: int = 0,
                  sample_period: float = 1 / 1712e6, delay_channels=None, sample_signed: bool = False,
                  out_int8: bool = False, out_scale: float = 1.0, t0: float = 0.0, batch_dt: float = 0.0,
-                 exact_coeffs: bool = False) -> None:
+                 exact_coeffs: bool = False, beam_weights: bool = False) -> None:
         for name, v in dict(n_batches=n_batches, n_channels_per_stream=n_channels_per_stream, n_channels=n_channels,
                             n_samples_per_channel=n_samples_per_channel, n_ants=n_ants, n_beams=n_beams).items():
             if int(v) <= 0:
@@ -69,12 +75,29 @@ class FusedBeamformerTemplate:
         self.t0 = float(t0)
         self.batch_dt = float(batch_dt)
         self.exact_coeffs = bool(exact_coeffs)
+        self.beam_weights = bool(beam_weights)
         self.flags = ((_lib.FUSED_SIGNED if self.sample_signed else 0) | (_lib.FUSED_OUT_INT8 if self.out_int8 else 0)
                       | (_lib.FUSED_EXACT_COEFF if self.exact_coeffs else 0))
         B, C, T, A, M = n_batches, n_channels_per_stream, n_samples_per_channel, n_ants, n_beams
         self.input_shape = (B, A, C, T, 2, 2)
         self.delay_shape = (delay_channels, M, A, 4)
         self.output_shape = (B, 2, C, T // 16, 16, 2 * M)
+        self.weights_shape = (M, A)
+
+    def check_weights(self, weights):
+        """Validate an (M, A) weight table for this configuration; returns it as float32.  The int8 output's
+        Q14 integer path needs rne(|g| * 2^14) <= 32639, i.e. |g| <= 1.992 (the high limb stays int8), and
+        2*A*max|g|*2^14*255 < 2^31 (no int32 overflow); the float path takes any finite weights."""
+        w = np.asarray(weights, np.float32)
+        if w.shape != self.weights_shape:
+            raise ValueError(f"beam weights must have shape {self.weights_shape}, got {w.shape}")
+        if not np.all(np.isfinite(w)):
+            raise ValueError("beam weights must be finite")
+        if self.out_int8:
+            g = float(np.max(np.abs(w))) if w.size else 0.0
+            if np.rint(g * 16384) > 32639 or 2 * self.n_ants * g * 16384 * 255 >= 2 ** 31:
+                raise ValueError(f"beam weight magnitude {g} out of range for int8 output with {self.n_ants} inputs")
+        return w
 
     def algorithmic_bytes(self):
         """HBM bytes one launch must move: voltages once, beams once, delay model once."""
@@ -99,10 +122,44 @@ class FusedBeamformer(accel.Operation):
         self.slots["inSamples"] = accel.IOSlot(t.input_shape, np.int8 if t.sample_signed else np.uint8)
         self.slots["delay_vals"] = accel.IOSlot(t.delay_shape, np.float32)
         self.slots["outData"] = accel.IOSlot(t.output_shape, np.int8 if t.out_int8 else np.float32)
+        self._weights = None
+        if t.beam_weights:
+            self.slots["beamWeights"] = accel.IOSlot(t.weights_shape, np.float32)
+            self._weights = np.ones(t.weights_shape, np.float32)
+            self._weights_dirty = True
+
+    def set_beam_weights(self, beam, *weights):
+        """`?beam-weights <beam> w_0 .. w_{A-1}` (corr3_servlet.py:140-153): set beam `beam`'s per-input weights.
+        Same reply condition as the servlet: the count must equal n_ants (ValueError here, FailReply there).
+        Takes effect from the next launch (stream-ordered upload)."""
+        t = self.template
+        if self._weights is None:
+            raise ValueError("operator was built without beam_weights=True")
+        if len(weights) == 1 and np.ndim(weights[0]) == 1:
+            weights = tuple(weights[0])
+        if len(weights) != t.n_ants:
+            raise ValueError(f"{len(weights)} weights received, expected {t.n_ants}")
+        if not 0 <= int(beam) < t.n_beams:
+            raise ValueError(f"beam {beam} out of range [0, {t.n_beams})")
+        new = self._weights.copy()
+        new[int(beam)] = np.asarray(weights, np.float32)
+        self._weights = t.check_weights(new)
+        self._weights_dirty = True
+
+    def beam_weights(self):
+        """The current (M, A) weight table (host copy)."""
+        return None if self._weights is None else self._weights.copy()
 
     def _run(self):
         t = self.template
-        _lib.call("bf_beamform_fused", self.buffer("inSamples").ptr, self.buffer("delay_vals").ptr, t.delay_channels,
-                  self.buffer("outData").ptr, t.n_batches, t.n_channels_per_stream, t.n_samples_per_channel,
-                  t.n_ants, t.n_beams, t.n_channels, t.xeng_id, float(t.sample_period), t.t0, t.batch_dt, t.flags,
-                  t.out_scale, self.command_queue.handle)
+        gains = None
+        if self._weights is not None:
+            buf = self.buffer("beamWeights")
+            if self._weights_dirty:
+                buf.set_async(self.command_queue, self._weights)
+                self._weights_dirty = False
+            gains = buf.ptr
+        _lib.call("bf_beamform_fused_weighted", self.buffer("inSamples").ptr, self.buffer("delay_vals").ptr,
+                  t.delay_channels, gains, self.buffer("outData").ptr, t.n_batches, t.n_channels_per_stream,
+                  t.n_samples_per_channel, t.n_ants, t.n_beams, t.n_channels, t.xeng_id, float(t.sample_period),
+                  t.t0, t.batch_dt, t.flags, t.out_scale, self.command_queue.handle)

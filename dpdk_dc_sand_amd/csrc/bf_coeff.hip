@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void coeff_gen_kernel(const float4* __restrict
     const int c = static_cast<int>(idx / (static_cast<long long>(M) * A));
     const float4 d = dv[(static_cast<size_t>(c) * M + m) * A + a];  // delay_vals[c][m][a]
     float re, im;
-    steering_coeff(d, static_cast<double>(base_ch + c), ctot, ts, 0.0, &re, &im);
+    steering_coeff(d, static_cast<double>(base_ch + c), make_phase(ctot, ts), 0.0, &re, &im);
     const float2 row0 = make_float2(re, im);   // W[2a][2m], W[2a][2m+1]
     const float2 row1 = make_float2(-im, re);  // W[2a+1][2m], W[2a+1][2m+1]
     for (int bp = 0; bp < B * P; ++bp) {
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void coeff_gen_time_kernel(const float4* __res
     const int cd = delay_channels == 1 ? 0 : c;
     const float4 d = dv[(static_cast<size_t>(cd) * M + m) * A + a];
     float re, im;
-    steering_coeff(d, static_cast<double>(base_ch + c), ctot, ts, t0 + t * dt_step, &re, &im);
+    steering_coeff(d, static_cast<double>(base_ch + c), make_phase(ctot, ts), t0 + t * dt_step, &re, &im);
     if constexpr (F16) {
       reinterpret_cast<__half2*>(out)[idx] = __floats2half2_rn(re, im);
     } else {

@@ -38,6 +38,7 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 struct FusedArgs {
   const uint8_t* raw;
   const float4* dv;
+  const float* gain;  // optional (M, A) real per-input beam weights (?beam-weights), folded into the phasors
   void* y;
   int delay_channels, B, C, T, A, M, S, NT, nslabs;
   long long base_ch;
@@ -90,6 +91,7 @@ template <int NTS>
 struct CoefPrefetch {
   static constexpr int kMaxPairs = (kGroup * 16 * 8 * NTS) / kThreads;  // S <= 4
   float4 dv[kMaxPairs];
+  float g[kMaxPairs];
 };
 
 template <int NTS>
@@ -104,7 +106,15 @@ __device__ __forceinline__ void load_delays(CoefPrefetch<NTS>& cp, const FusedAr
     a = a < P.A ? a : P.A - 1;
     m = m < P.M ? m : P.M - 1;
     cp.dv[j] = P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a];
+    cp.g[j] = 1.0f;
+    if (P.gain) cp.g[j] = P.gain[m * P.A + a];  // uniform branch; absent gains cost nothing
   }
+}
+
+// Per-(a, m) real beam weight applied to the float32 phasor (one rounding per component, as the oracle).
+__device__ __forceinline__ void apply_gain(float g, float* re, float* im) {
+  *re = __fmul_rn(*re, g);
+  *im = __fmul_rn(*im, g);
 }
 
 template <bool Exact, int Mode, int NTS>
@@ -127,10 +137,11 @@ __device__ __forceinline__ void make_coefs(_Float16* lh, const CoefPrefetch<NTS>
       im = 0.25f - 1e-3f * m;
     } else if (a < P.A && m < P.M) {
       if constexpr (Exact) {
-        steering_coeff(cp.dv[j], ch, P.ctot, P.ts, dt, &re, &im);
+        steering_coeff(cp.dv[j], ch, make_phase(P.ctot, P.ts), dt, &re, &im);
       } else {
         steering_coeff_fast(cp.dv[j], chc, P.k, dt, &re, &im);
       }
+      if (P.gain) apply_gain(cp.g[j], &re, &im);
     }
     const int cl = 2 * ml;
     put_split(lh, coef_elem(2 * a, cl, nts), re);          // W[2a][2m]     =  cos
@@ -157,10 +168,11 @@ __device__ __forceinline__ void gen_coefs(_Float16* lh, const FusedArgs& P, int 
     if (a < P.A && m < P.M) {
       const float4 d = P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a];
       if constexpr (Exact) {
-        steering_coeff(d, ch, P.ctot, P.ts, dt, &re, &im);
+        steering_coeff(d, ch, make_phase(P.ctot, P.ts), dt, &re, &im);
       } else {
         steering_coeff_fast(d, chc, P.k, dt, &re, &im);
       }
+      if (P.gain) apply_gain(P.gain[m * P.A + a], &re, &im);
     }
     const int cl = 2 * ml;
     put_split(lh, coef_elem(2 * a, cl, nts), re);
@@ -556,8 +568,11 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P
       const int a = e / nbeam, ml = e - a * nbeam;
       const int m = tau0 * 8 + ml;
       float re = 0.0f, im = 0.0f;
-      if (a < P.A && m < P.M)
-        steering_coeff(P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a], ch, P.ctot, P.ts, dt, &re, &im);
+      if (a < P.A && m < P.M) {
+        steering_coeff(P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a], ch, make_phase(P.ctot, P.ts), dt, &re,
+                       &im);
+        if (P.gain) apply_gain(P.gain[m * P.A + a], &re, &im);
+      }
       const int cl = 2 * ml;
       put_q14(lb, colsum, 2 * a, cl, nts, re);
       put_q14(lb, colsum, 2 * a, cl + 1, nts, im);
@@ -769,8 +784,9 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
         if constexpr (Mode & 16) {
           steering_coeff_fast(cp.dv[j], ch - P.ctot / 2.0, P.k, dt, &re, &im);
         } else {
-          steering_coeff(cp.dv[j], ch, P.ctot, P.ts, dt, &re, &im);
+          steering_coeff(cp.dv[j], ch, make_phase(P.ctot, P.ts), dt, &re, &im);
         }
+        if (P.gain) apply_gain(cp.g[j], &re, &im);
       }
       const int cl = 2 * ml;
       const int Wc = static_cast<int>(__builtin_rintf(re * 16384.0f));
@@ -1068,6 +1084,14 @@ int dispatch(FusedArgs P, hipStream_t st) {
 extern "C" int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, int delay_channels, void* y, int B,
                                  int C, int T, int A, int M, int Ctot, int xeng_id, double sample_period, double t0,
                                  double batch_dt, int flags, float out_scale, void* stream) {
+  return bf_beamform_fused_weighted(raw, delay_vals, delay_channels, nullptr, y, B, C, T, A, M, Ctot, xeng_id,
+                                    sample_period, t0, batch_dt, flags, out_scale, stream);
+}
+
+extern "C" int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay_vals, int delay_channels,
+                                          const float* gains, void* y, int B, int C, int T, int A, int M, int Ctot,
+                                          int xeng_id, double sample_period, double t0, double batch_dt, int flags,
+                                          float out_scale, void* stream) {
   BF_REQUIRE(raw && delay_vals && y, "bf_beamform_fused: null pointer");
   BF_REQUIRE(B > 0 && C > 0 && T > 0 && A > 0 && M > 0 && Ctot > 0 && xeng_id >= 0,
              "bf_beamform_fused: bad shape B=%d C=%d T=%d A=%d M=%d Ctot=%d", B, C, T, A, M, Ctot);
@@ -1082,6 +1106,7 @@ extern "C" int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, in
   bf::FusedArgs P{};
   P.raw = raw;
   P.dv = reinterpret_cast<const float4*>(delay_vals);
+  P.gain = gains;
   P.y = y;
   P.delay_channels = delay_channels;
   P.B = B;

@@ -116,6 +116,18 @@ int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, int delay_cha
                       int T, int A, int M, int Ctot, int xeng_id, double sample_period, double t0,
                       double batch_dt, int flags, float out_scale, void* stream);
 
+/* bf_beamform_fused with per-input beam weights folded into the phasors (control-plane hook: the
+ * `?beam-weights <beam> w_0 .. w_{A-1}` request, ngkcs/ngkcs/corr3_servlet.py:140-153, forwarded to the
+ * B-engines).  gains: f32 (M, A) real weight of antenna a in beam m on the device, or NULL (= all ones, exactly
+ * bf_beamform_fused).  Coefficient (a, m) becomes (g*cos, g*sin), one float32 rounding per component.  With
+ * BF_FUSED_OUT_INT8 the Q14 integer path needs |g| <= 1.992 (the high limb stays int8) and
+ * 2*A*max|g|*2^14*255 < 2^31 (no int32 overflow); the Python wrapper, which owns the host copy of the weights,
+ * checks both. */
+int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay_vals, int delay_channels, const float* gains,
+                               void* y, int B, int C, int T, int A, int M, int Ctot, int xeng_id,
+                               double sample_period, double t0, double batch_dt, int flags, float out_scale,
+                               void* stream);
+
 /* 8-bit requantiser (no reference counterpart; SURVEY §7 build step 7): q = clamp(rne(y*scale), -127, 127). */
 int bf_requant(const float* y, int8_t* q, size_t n, float scale, void* stream);
 

@@ -118,19 +118,24 @@ def op_sequence(raw, delay_vals, C, Ctot, A, M, xeng_id=0, Ts=TS_MEERKAT):
     return complex_mult(reorder(raw), coeffs(delay_vals, B, 2, C, Ctot, A, M, xeng_id, Ts))
 
 
-def fused_beamform(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, signed=False):
+def fused_beamform(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, signed=False, gains=None):
     """The fused MI355X operator's contract: reorder + per-batch coefficient regeneration + complex mult.
 
     raw: (B, A, C, T, 2, 2) 8-bit; delay_vals: (C, M, A, 4) or compact (1, M, A, 4) (same model for every
     channel).  Batch b uses coefficients at dt_b = t0 + b * batch_dt (the per-block regeneration of
-    BeamformerParameters.h:17 ACCUMULATIONS_BEFORE_NEW_COEFFS).  Output f32 (B, 2, C, T/16, 16, 2M)."""
+    BeamformerParameters.h:17 ACCUMULATIONS_BEFORE_NEW_COEFFS).  gains: optional (M, A) real beam weights
+    (see fused_tables).  Output f32 (B, 2, C, T/16, 16, 2M)."""
     B, A, C, T, P, Z = raw.shape
-    w = fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt)
+    w = fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt, gains)
     return complex_mult(reorder(raw), w, signed=signed)
 
 
-def fused_tables(delay_vals, B, C, Ctot, A, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0):
-    """The (B, 2, C, 2A, 2M) coefficient tables the fused operator applies (batch b at dt = t0 + b*batch_dt)."""
+def fused_tables(delay_vals, B, C, Ctot, A, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, gains=None):
+    """The (B, 2, C, 2A, 2M) coefficient tables the fused operator applies (batch b at dt = t0 + b*batch_dt).
+
+    gains: optional (M, A) float32 per-input beam weights (the `?beam-weights <beam> w_0..w_{A-1}` control request,
+    ngkcs/ngkcs/corr3_servlet.py:140-153): the float32 phasor of (a, m) is scaled by g[m, a] in float32, one
+    rounding per component, before the [[R, I], [-I, R]] packing."""
     d = np.asarray(delay_vals, np.float32)
     if d.shape[0] == 1 and C > 1:
         d = np.broadcast_to(d, (C,) + d.shape[1:])
@@ -138,6 +143,10 @@ def fused_tables(delay_vals, B, C, Ctot, A, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, ba
     w = np.empty((B, 2, C, 2 * A, 2 * M), np.float32)
     for b in range(B):
         cos, sin = coeffs_at(d, C, Ctot, A, M, xeng_id, Ts, t0 + b * batch_dt)
+        if gains is not None:
+            g = np.asarray(gains, np.float32)
+            assert g.shape == (M, A), g.shape
+            cos, sin = cos * g, sin * g  # float32 x float32 -> float32
         w[b] = _pack_blocks(cos, sin, 1, 2)[0]
     return w
 
@@ -165,14 +174,14 @@ def quantise_coeffs(w):
 
 
 def fused_beamform_int8(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, scale=1.0,
-                        signed=False):
+                        signed=False, gains=None):
     """Contract of the fused operator's int8 (requantised) output -- bit-exact:
         W = rne(w * 2^14)  (w: the exact float32 coefficients of fused_tables, i.e. CoeffGenerator's at dt = 0)
         y = sum_k x_k W_k  (exact integers)
         q = clamp(rne(float32(y) * float32(float32(scale) * 2^-14)), -127, 127)
     raw: (B, A, C, T, 2, 2) 8-bit -> int8 (B, 2, C, T/16, 16, 2M)."""
     B, A, C, T, P, Z = raw.shape
-    W = quantise_coeffs(fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt))
+    W = quantise_coeffs(fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt, gains))
     xr = reorder(raw)
     X = (xr.view(np.int8) if signed else xr).astype(np.int64).reshape(B, 2, C, T, 2 * A)
     Y = np.matmul(X, W)

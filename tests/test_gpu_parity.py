@@ -341,3 +341,59 @@ def test_errors_raise(context, command_queue):
     op = MatrixMultiplyTemplate(context, 4, 2, 32, 1, 1).instantiate(command_queue)
     with pytest.raises(ValueError):
         op.bind(inData=accel.DeviceArray(context, (3,), np.uint8))
+
+
+@pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
+    (64, 16, 3, 256, 2, 1, True), (19, 3, 4, 48, 2, 4, False), (130, 9, 2, 64, 1, 1, True), (33, 8, 2, 64, 2, 2, False)])
+@pytest.mark.parametrize("exact", [False, True])
+def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, T, B, dch, signed):
+    """?beam-weights (corr3_servlet.py:140-153): per-(beam, input) weights folded into the phasors, set through the
+    request-shaped API, against the oracle's weighted tables (float path: f32-class tolerance)."""
+    Ctot, xeng, t0, bdt = 4096, 1, 1e-3, 256 * 8192 * TS
+    d = random_delays(dch, M, A, A + 7 * M)
+    rng = np.random.default_rng(A * 5 + M)
+    raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8)
+    if signed:
+        raw = raw.view(np.int8)
+    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=dch, sample_signed=signed,
+                                 t0=t0, batch_dt=bdt, exact_coeffs=exact, beam_weights=True).instantiate(command_queue)
+    g = rng.uniform(-1.5, 1.5, (M, A)).astype(np.float32)
+    g[0, : A // 2] = 0.0  # switched-off inputs
+    for m in range(M):
+        fu.set_beam_weights(m, *g[m])
+    (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    ref = O.fused_beamform(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, signed=signed, gains=g)
+    w = O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, t0=t0, batch_dt=bdt, gains=g)
+    assert_beams_allclose(y, ref, O.reorder(raw), w, signed=signed)
+    fu.set_beam_weights(M - 1, *np.ones(A))  # a later request takes effect on the next launch
+    g[M - 1] = 1.0
+    fu()
+    y2 = fu.buffer("outData").get(command_queue)
+    ref2 = O.fused_beamform(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, signed=signed, gains=g)
+    w2 = O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, t0=t0, batch_dt=bdt, gains=g)
+    assert_beams_allclose(y2, ref2, O.reorder(raw), w2, signed=signed)
+
+
+@pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
+    (64, 16, 3, 256, 2, 1, True), (64, 16, 2, 256, 2, 1, False), (19, 3, 4, 48, 2, 4, False),
+    (130, 9, 2, 64, 1, 1, True)])
+@pytest.mark.parametrize("i8_kernel", ["item", "generic"])
+def test_fused_int8_beam_weights_bit_exact(context, command_queue, monkeypatch, i8_kernel, A, M, C, T, B, dch, signed):
+    """Weighted int8 beams: Q14 limbs of the weighted float32 coefficients, bit-exact to the integer contract."""
+    monkeypatch.setenv("BF_FUSED_KERNEL", i8_kernel)
+    Ctot, xeng, t0, bdt = 4096, 2, 1e-3, 256 * 8192 * TS
+    d = random_delays(dch, M, A, A * 3 + M)
+    rng = np.random.default_rng(A * 11 + C)
+    raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8)
+    if signed:
+        raw = raw.view(np.int8)
+    g = rng.uniform(-1.9, 1.9, (M, A)).astype(np.float32)
+    op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=dch, sample_signed=signed,
+                                 out_int8=True, out_scale=1 / 64, t0=t0, batch_dt=bdt,
+                                 beam_weights=True).instantiate(command_queue)
+    for m in range(M):
+        op.set_beam_weights(m, g[m])
+    (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    ref = O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, scale=1 / 64, signed=signed, gains=g)
+    np.testing.assert_array_equal(q, ref)
+    assert np.abs(ref.astype(int)).max() >= 4

@@ -97,3 +97,30 @@ def test_compound_slot_rejects_mismatched_children():
 def test_dimension_and_slot_sizes():
     s = accel.IOSlot((accel.Dimension(4, exact=True), 5), np.float32)
     assert s.shape == (4, 5) and s.required_bytes() == 80
+
+
+def test_beam_weights_request_semantics():
+    """`?beam-weights <beam> w_0..w_{A-1}` (corr3_servlet.py:140-153): the count must equal n_ants; the table starts
+    at ones; updates are per beam; int8 output bounds the magnitude (Q14 limbs, int32 accumulator)."""
+    t = FusedBeamformerTemplate(None, 1, 4, 4, 16, 5, 3, delay_channels=1, beam_weights=True)
+    op = t.instantiate(FakeQueue())
+    assert op.slots["beamWeights"].shape == (3, 5)
+    np.testing.assert_array_equal(op.beam_weights(), np.ones((3, 5), np.float32))
+    op.set_beam_weights(1, 0.5, 0.25, 1, 2, 3)
+    op.set_beam_weights(2, np.arange(5))
+    w = op.beam_weights()
+    np.testing.assert_array_equal(w[0], 1)
+    np.testing.assert_array_equal(w[1], [0.5, 0.25, 1, 2, 3])
+    np.testing.assert_array_equal(w[2], np.arange(5))
+    with pytest.raises(ValueError, match="4 weights received, expected 5"):
+        op.set_beam_weights(0, 1, 1, 1, 1)
+    with pytest.raises(ValueError):
+        op.set_beam_weights(3, *[1] * 5)
+    with pytest.raises(ValueError):
+        op.set_beam_weights(0, 1, 1, np.nan, 1, 1)
+    i8 = FusedBeamformerTemplate(None, 1, 4, 4, 16, 5, 3, out_int8=True, beam_weights=True).instantiate(FakeQueue())
+    i8.set_beam_weights(0, 1.992, -1.992, 0, 0, 0)
+    with pytest.raises(ValueError, match="out of range"):
+        i8.set_beam_weights(0, 2.0, 0, 0, 0, 0)
+    with pytest.raises(ValueError, match="without beam_weights"):
+        FusedBeamformerTemplate(None, 1, 4, 4, 16, 5, 3).instantiate(FakeQueue()).set_beam_weights(0, *[1] * 5)

@@ -99,3 +99,26 @@ def test_int8_contract_is_close_to_float_beams():
     qf = O.requantise(O.fused_beamform(raw, d, Ctot), 1 / 16).astype(int)
     assert np.abs(q - qf).max() <= 1
     assert (q == qf).mean() > 0.99
+
+
+def test_beam_weights_oracle_properties():
+    """Weights of one are the identity; power-of-two weights scale beams exactly (linearity); weights are per
+    (beam, input): zeroing input a of beam m removes exactly antenna a's contribution to beam m."""
+    rng = np.random.default_rng(5)
+    raw = O.u8_voltages((2, 6, 3, 32, 2, 2), seed=9)
+    d = np.zeros((1, 4, 6, 4), np.float32)
+    d[..., 0] = rng.uniform(0, 10 * O.TS_MEERKAT, (1, 4, 6))
+    d[..., 2] = rng.uniform(-np.pi, np.pi, (1, 4, 6))
+    base = O.fused_beamform(raw, d, 64)
+    np.testing.assert_array_equal(O.fused_beamform(raw, d, 64, gains=np.ones((4, 6), np.float32)), base)
+    np.testing.assert_array_equal(O.fused_beamform(raw, d, 64, gains=np.full((4, 6), 0.25, np.float32)), base * 0.25)
+    g = np.ones((4, 6), np.float32)
+    g[2, 3] = 0.0
+    only = raw.copy()
+    only[:, [a for a in range(6) if a != 3]] = 0  # antenna 3 alone
+    diff = base - O.fused_beamform(raw, d, 64, gains=g)
+    contrib = O.fused_beamform(only, d, 64)
+    np.testing.assert_allclose(diff[..., 4:6], contrib[..., 4:6], rtol=1e-5, atol=1e-3)  # beam 2 = cols 4, 5
+    np.testing.assert_array_equal(diff[..., :4], 0)
+    q1 = O.fused_beamform_int8(raw, d, 64, scale=1 / 16)
+    np.testing.assert_array_equal(O.fused_beamform_int8(raw, d, 64, scale=1 / 16, gains=np.ones((4, 6), np.float32)), q1)

@@ -19,8 +19,12 @@ B, C, T, A, M = [int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (8, 40
 nin = B * A * C * T * 4
 nout = B * 2 * C * T * 2 * M * 4
 bufs = [(accel.DeviceArray(ctx, (nin,), np.uint8), accel.DeviceArray(ctx, (nout,), np.uint8)) for _ in range(2)]
-for xi, yo in bufs:
-    _lib.call("bf_memset", xi.ptr, 7, nin, q.handle)
+_rng = np.random.default_rng(1)
+for xi, yo in bufs:  # random voltages: constant data runs at a higher clock (MI355X_MICROARCH.md) and flatters
+    if _os.environ.get("DIAG_CONST", "0") == "1":
+        _lib.call("bf_memset", xi.ptr, 7, nin, q.handle)
+    else:
+        xi.set(q, _rng.integers(0, 256, nin, dtype=np.uint8))
 dv = accel.DeviceArray(ctx, (M * A * 4,), np.float32)
 dv.set(q, np.random.default_rng(0).uniform(0, 1e-8, M * A * 4).astype(np.float32))
 alg = nin + nout
