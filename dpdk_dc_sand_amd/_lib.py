@@ -14,7 +14,9 @@ LIB_PATH = os.path.join(_HERE, "libbf.so")
 
 c_int, c_float, c_double, c_size_t, c_void_p, c_char_p = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
                                                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p)
+c_longlong = ctypes.c_longlong
 P_int, P_float, P_void = ctypes.POINTER(c_int), ctypes.POINTER(c_float), ctypes.POINTER(c_void_p)
+P_size_t, P_longlong = ctypes.POINTER(c_size_t), ctypes.POINTER(c_longlong)
 
 # name -> (restype, argtypes); mirrors include/bf.h (tests/test_abi.py checks the two agree).
 PROTOTYPES = {
@@ -54,6 +56,17 @@ PROTOTYPES = {
     "bf_beamform_fused_weighted": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                            c_int, c_int, c_int, c_double, c_double, c_double, c_int, c_float,
                                            c_void_p]),
+    "bf_pipeline_create": (c_int, [P_void, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_int,
+                                   c_float, c_int, c_int]),
+    "bf_pipeline_destroy": (c_int, [c_void_p]),
+    "bf_pipeline_frame_bytes": (c_int, [c_void_p, P_size_t, P_size_t]),
+    "bf_pipeline_set_delays": (c_int, [c_void_p, c_void_p]),
+    "bf_pipeline_set_gains": (c_int, [c_void_p, c_void_p]),
+    "bf_pipeline_submit": (c_int, [c_void_p, c_void_p, c_void_p, c_double, c_double, P_longlong]),
+    "bf_pipeline_wait": (c_int, [c_void_p, c_longlong, c_int]),
+    "bf_pipeline_query": (c_int, [c_void_p, c_longlong, c_int, P_int]),
+    "bf_pipeline_flush": (c_int, [c_void_p]),
+    "bf_pipeline_stage_ms": (c_int, [c_void_p, c_longlong, P_float, P_float, P_float]),
     "bf_requant": (c_int, [c_void_p, c_void_p, c_size_t, c_float, c_void_p]),
     "bf_fused_algorithmic_bytes": (c_double, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
 }

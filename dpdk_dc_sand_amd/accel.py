@@ -160,6 +160,49 @@ class Dimension:
         return f"Dimension({self.size})"
 
 
+class _PinnedAllocation:
+    """Owner of one bf_host_alloc (hipHostMalloc) block; freed when the last array view goes away."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        _lib.call("bf_host_alloc", ctypes.byref(p), max(self.nbytes, 1))
+        self.ptr = p.value
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            try:
+                _lib.load().bf_host_free(self.ptr)
+            except Exception:
+                pass
+            self.ptr = None
+
+
+class HostArray(np.ndarray):
+    """Page-locked host array (katsdpsigproc accel.HostArray): the host side of asynchronous copies and of the
+    streaming pipeline's frames, so DMA can overlap compute.  A numpy array in every other respect; views keep
+    the allocation alive."""
+
+    def __new__(cls, shape, dtype, context=None):
+        shape = tuple(int(s) for s in (shape if np.ndim(shape) else (shape,)))
+        dtype = np.dtype(dtype)
+        count = int(np.prod(shape, dtype=np.int64))
+        if context is not None:
+            context.activate()
+        alloc = _PinnedAllocation(count * dtype.itemsize)
+        raw = (ctypes.c_uint8 * max(count * dtype.itemsize, 1)).from_address(alloc.ptr)
+        obj = np.frombuffer(raw, dtype=dtype, count=count).reshape(shape).view(cls)
+        obj._alloc = alloc
+        return obj
+
+    def __array_finalize__(self, obj):
+        self._alloc = getattr(obj, "_alloc", None)
+
+    @property
+    def ptr(self):
+        return self.ctypes.data
+
+
 class DeviceArray:
     """Device buffer with numpy-like metadata (katsdpsigproc accel.DeviceArray subset)."""
 

@@ -55,7 +55,8 @@ int bf_device_name(int device, char* buf, size_t len) {
   BF_REQUIRE(buf != nullptr && len > 0, "bf_device_name: empty buffer");
   hipDeviceProp_t prop;
   BF_HIP(hipGetDeviceProperties(&prop, device));
-  snprintf(buf, len, "%s (%s, %d CUs)", prop.name, prop.gcnArchName, prop.multiProcessorCount);
+  const char* name = prop.name[0] ? prop.name : "AMD Instinct GPU";  // the marketing name can be empty
+  snprintf(buf, len, "%s (%s, %d CUs)", name, prop.gcnArchName, prop.multiProcessorCount);
   return BF_OK;
 }
 

@@ -131,6 +131,29 @@ int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay_vals, int 
 /* 8-bit requantiser (no reference counterpart; SURVEY §7 build step 7): q = clamp(rne(y*scale), -127, 127). */
 int bf_requant(const float* y, int8_t* q, size_t n, float scale, void* stream);
 
+/* ---- streaming ingest --------------------------------------------------------
+ * Pinned host frames -> H2D stream -> bf_beamform_fused_weighted on a compute stream -> D2H stream, over a ring of
+ * `depth` device slots; the phases of successive frames overlap.  Replaces the back-to-back HtoD / kernel / DtoH
+ * phases of the reference harness (common/UnitTest.cpp:28-57) and the event-chained PCIe loop
+ * (utilities/pcie_bandwidth_tests/cudaPcieRateTest.cpp:63-123).  Frames have the fused operator's shapes: in
+ * (B, A, C, T, 2, 2) 8-bit, out (B, 2, C, T/16, 16, 2M) f32 or int8.  Host buffers should be pinned
+ * (bf_host_alloc) for the copies to overlap; they must stay untouched until bf_pipeline_wait(ticket, 0) (input)
+ * / (ticket, 1) (output).  The pipeline lives on the device current at creation; calls restore the caller's device.
+ * Delay-model and weight updates apply to every frame submitted after them (stream-ordered uploads). */
+typedef struct bf_pipeline bf_pipeline;
+int bf_pipeline_create(bf_pipeline** out, int B, int C, int T, int A, int M, int Ctot, int xeng_id,
+                       double sample_period, int flags, float out_scale, int delay_channels, int depth);
+int bf_pipeline_destroy(bf_pipeline* p);
+int bf_pipeline_frame_bytes(const bf_pipeline* p, size_t* in_bytes, size_t* out_bytes);
+int bf_pipeline_set_delays(bf_pipeline* p, const float* host_delay_vals);  /* host f32 (Cd, M, A, 4) */
+int bf_pipeline_set_gains(bf_pipeline* p, const float* host_gains);        /* host f32 (M, A); NULL = unit */
+int bf_pipeline_submit(bf_pipeline* p, const void* host_in, void* host_out, double t0, double batch_dt,
+                       long long* ticket);
+int bf_pipeline_wait(bf_pipeline* p, long long ticket, int stage);         /* stage 0 input, 1 output */
+int bf_pipeline_query(bf_pipeline* p, long long ticket, int stage, int* done);
+int bf_pipeline_flush(bf_pipeline* p);
+int bf_pipeline_stage_ms(bf_pipeline* p, long long ticket, float* h2d_ms, float* compute_ms, float* d2h_ms);
+
 /* Algorithmic HBM bytes of one bf_beamform_fused launch (bench / roofline bookkeeping). */
 double bf_fused_algorithmic_bytes(int B, int C, int T, int A, int M, int delay_channels, int out_int8);
 

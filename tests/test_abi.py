@@ -74,3 +74,16 @@ def test_algorithmic_bytes():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(OSError, match="no CPU fallback"):
         _lib.load(str(tmp_path / "libbf.so"))
+
+
+def test_pipeline_argument_validation_without_gpu():
+    h = ctypes.c_void_p()
+    with pytest.raises(_lib.BeamformerError, match="depth"):
+        _lib.call("bf_pipeline_create", ctypes.byref(h), 1, 4, 16, 4, 1, 64, 0, 1e-9, 0, 1.0, 1, 0)
+    with pytest.raises(_lib.BeamformerError, match="multiple of 16"):
+        _lib.call("bf_pipeline_create", ctypes.byref(h), 1, 4, 17, 4, 1, 64, 0, 1e-9, 0, 1.0, 1, 2)
+    with pytest.raises(_lib.BeamformerError, match="null pointer"):
+        _lib.call("bf_pipeline_create", None, 1, 4, 16, 4, 1, 64, 0, 1e-9, 0, 1.0, 1, 2)
+    with pytest.raises(_lib.BeamformerError, match="null pipeline"):
+        _lib.call("bf_pipeline_wait", None, 0, 1)
+    assert _lib.load().bf_pipeline_destroy(None) == 0

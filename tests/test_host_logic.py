@@ -124,3 +124,11 @@ def test_beam_weights_request_semantics():
         i8.set_beam_weights(0, 2.0, 0, 0, 0, 0)
     with pytest.raises(ValueError, match="without beam_weights"):
         FusedBeamformerTemplate(None, 1, 4, 4, 16, 5, 3).instantiate(FakeQueue()).set_beam_weights(0, *[1] * 5)
+
+
+def test_streaming_template():
+    from dpdk_dc_sand_amd.beamforming import StreamingBeamformerTemplate
+    t = StreamingBeamformerTemplate(None, 2, 8, 64, 32, 4, 3, delay_channels=1, batch_dt=1e-3, out_int8=True, depth=3)
+    assert (t.depth, t.frame_dt, t.input_shape, t.flags) == (3, 2e-3, (2, 4, 8, 32, 2, 2), 2)
+    with pytest.raises(ValueError):
+        StreamingBeamformerTemplate(None, 2, 8, 64, 32, 4, 3, depth=0)
