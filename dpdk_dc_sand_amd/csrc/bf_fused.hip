@@ -40,7 +40,7 @@ struct FusedArgs {
   const float4* dv;
   const float* gain;  // optional (M, A) real per-input beam weights (?beam-weights), folded into the phasors
   void* y;
-  int delay_channels, B, C, T, A, M, S, NT, nslabs;
+  int delay_channels, B, C, T, A, M, S, NT, nslabs, xcd_order;
   long long base_ch;
   double ctot, ts, k, t0, batch_dt;
   float out_scale;
@@ -448,8 +448,19 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
-  const int slab = blockIdx.x % P.nslabs;
-  const int bc = blockIdx.x / P.nslabs;
+  // XCD-aware order: workgroup g runs on XCD g % 8, so the nslabs beam slabs of item (b, c) are given to blocks
+  // g = 8 (nslabs * j + slab) + x on the same XCD x: they run back to back there and the slabs after the first
+  // re-read the item's voltages from that XCD's L2 instead of HBM.
+  int slab, bc;
+  if (P.xcd_order) {
+    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
+    slab = local % P.nslabs;
+    bc = (local / P.nslabs) * 8 + x;
+    if (bc >= P.B * P.C) return;
+  } else {
+    slab = blockIdx.x % P.nslabs;
+    bc = blockIdx.x / P.nslabs;
+  }
   const int b = bc / P.C, c = bc % P.C;
   const int tau0 = slab * NTS;
   const int nts = min(NTS, P.NT - tau0);
@@ -1047,7 +1058,10 @@ int launch_generic(FusedArgs P, hipStream_t st) {
   P.nslabs = (P.NT + NTS - 1) / NTS;
   const size_t lds = coef_lds_bytes(P.S, NTS);
   BF_REQUIRE(lds <= kMaxLds, "bf_beamform_fused: n_ants=%d too large", P.A);
-  const long long grid = static_cast<long long>(P.B) * P.C * P.nslabs;
+  const char* xo = getenv("BF_FUSED_XCD_ORDER");
+  P.xcd_order = P.nslabs > 1 && !(xo && xo[0] == '0');
+  const long long items = static_cast<long long>(P.B) * P.C;
+  const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
   hipLaunchKernelGGL((beamform_fused_kernel<Signed, OutI8, NTS, Exact>), dim3(static_cast<unsigned>(grid)),
                      dim3(kThreads), lds, st, P);
@@ -1075,7 +1089,10 @@ int dispatch(FusedArgs P, hipStream_t st) {
     if (M2 == 16) return launch_item<Signed, OutI8, 1, Exact, true>(P, st);
     return launch_item<Signed, OutI8, 1, Exact, false>(P, st);
   }
-  if (P.NT >= 2 && coef_lds_bytes(P.S, 2) <= kMaxLds) return launch_generic<Signed, OutI8, 2, Exact>(P, st);
+  const char* wn = getenv("BF_FUSED_GENERIC_NTS");  // measurement: force the slab width
+  const int want = wn ? atoi(wn) : 2;
+  if (want >= 4 && P.NT >= 4 && coef_lds_bytes(P.S, 4) <= kMaxLds) return launch_generic<Signed, OutI8, 4, Exact>(P, st);
+  if (want >= 2 && P.NT >= 2 && coef_lds_bytes(P.S, 2) <= kMaxLds) return launch_generic<Signed, OutI8, 2, Exact>(P, st);
   return launch_generic<Signed, OutI8, 1, Exact>(P, st);
 }
 
