@@ -39,6 +39,9 @@ WORKLOADS = {
                  "per-batch coefficient regeneration fused (BASELINE configs[2])"),
     "cfg2": dict(A=64, M=1, C=4096, T=256, B=8, desc="64 ants, 1 beam, 4096 ch/GPU, T=256, B=8, dual-pol int8 "
                  "(BASELINE configs[1])"),
+    "cfg4": dict(A=256, M=64, C=4096, T=256, B=1, Ctot=32768,
+                 desc="256 ants, 64 beams, 4096 of 32768 ch per GPU (X-engine = rank), T=256, B=1, dual-pol int8 "
+                      "(BASELINE configs[3], per GPU)"),
 }
 
 
@@ -112,7 +115,7 @@ def run_gpu(args, dist, wl):
     ctx = accel.create_some_context(device=dist.local_rank % n_dev)
     queue = ctx.create_command_queue()
     A, M, C, T, B = wl["A"], wl["M"], wl["C"], wl["T"], wl["B"]
-    Ctot = C * max(dist.world, 1)
+    Ctot = wl.get("Ctot", C * max(dist.world, 1))
     tmpl = FusedBeamformerTemplate(ctx, B, C, Ctot, T, A, M, xeng_id=dist.rank, sample_period=TS, delay_channels=1,
                                    sample_signed=True, out_int8=args.out_int8, out_scale=1 / 64,
                                    t0=0.0, batch_dt=T * 2 * Ctot * TS)
@@ -174,7 +177,8 @@ def cpu_baseline(wl, seconds=10.0):
     def once(c):
         raw = rng.integers(-128, 128, size=(B, A, c, T, 2, 2), dtype=np.int8)
         t = time.perf_counter()
-        O.fused_beamform(raw, d, wl["C"], signed=True, batch_dt=T * 2 * wl["C"] * TS)
+        Ctot = wl.get("Ctot", wl["C"])
+        O.fused_beamform(raw, d, Ctot, signed=True, batch_dt=T * 2 * Ctot * TS)
         return time.perf_counter() - t
 
     c = 16
@@ -221,12 +225,20 @@ KERNELS = {False: ("beamform_fused_item_kernel",
                   "Q14 two-limb int8 coefficients on v_mfma_i32_16x16x64_i8, exact int32 accumulation, int8 beams")}
 
 
+def kernel_name(wl, out_int8):
+    """The launch's dominant kernel (bf_fused.hip dispatch): item kernels for A <= 64 and T <= 256, else the wide
+    kernel (f32 beams) / the generic integer kernel (int8 beams)."""
+    if wl["A"] <= 64 and wl["T"] <= 256:
+        return KERNELS[out_int8][0]
+    return "beamform_fused_i8_kernel" if out_int8 else "beamform_fused_wide_kernel"
+
+
 def secondary(args, dist, workload, out_int8):
     sub = argparse.Namespace(**{**vars(args), "workload": workload, "out_int8": out_int8})
     r = run_gpu(sub, dist, WORKLOADS[workload])
     r.pop("out")
     return {"workload": workload + ": " + WORKLOADS[workload]["desc"], "output": "int8" if out_int8 else "float32",
-            "kernel": KERNELS[out_int8][0],
+            "kernel": kernel_name(WORKLOADS[workload], out_int8),
             "value": round(r["samples_per_step"] * args.steps / r["t_max"] / 1e9, 2), "unit": "Gsamples/s",
             "roofline_frac": round(r["alg_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
             "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"]}
@@ -258,14 +270,14 @@ def main():
         "device": r["device"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": KERNELS[args.out_int8][0], "avg_launch_us": round(r["kernel_s"] * 1e6, 2),
+                     "kernel": kernel_name(wl, args.out_int8), "avg_launch_us": round(r["kernel_s"] * 1e6, 2),
                      "alg_bytes_per_launch": r["alg_bytes"]},
         "cpu_baseline": None,
     }
     del ops_queue
     if dist.rank == 0 and dist.world == 1 and not args.no_secondary and args.workload == "cfg3":
         line["secondary"] = []
-        for workload, out_int8 in (("cfg2", args.out_int8), ("cfg3", not args.out_int8)):
+        for workload, out_int8 in (("cfg2", args.out_int8), ("cfg3", not args.out_int8), ("cfg4", args.out_int8)):
             try:
                 line["secondary"].append(secondary(args, dist, workload, out_int8))
             except Exception as e:  # secondary lines are informational

@@ -20,8 +20,7 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "bf_mfma.hpp"
-#include "bf_phase.hpp"
+#include "bf_fused.hpp"
 
 namespace bf {
 
@@ -33,18 +32,6 @@ constexpr int kSkipCoef = 1, kSkipMfma = 2, kSkipStore = 4, kSkipLoad = 8;
 // time, profiles/r1_v2_ablation_nt.txt); kCachedLoad selects plain loads, kNtStore non-temporal beam stores
 // (slower: +17 %).
 constexpr int kCachedLoad = 128, kNtStore = 256;
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-
-struct FusedArgs {
-  const uint8_t* raw;
-  const float4* dv;
-  const float* gain;  // optional (M, A) real per-input beam weights (?beam-weights), folded into the phasors
-  void* y;
-  int delay_channels, B, C, T, A, M, S, NT, nslabs, xcd_order;
-  long long base_ch;
-  double ctot, ts, k, t0, batch_dt;
-  float out_scale;
-};
 
 // One group of 4 k-steps: 16 x 16-byte loads per lane, all UNCONDITIONAL: out-of-range antennas (a >= A) read
 // antenna A-1 and meet zero coefficient rows, out-of-range time quads read the last quad and are never stored,
@@ -109,12 +96,6 @@ __device__ __forceinline__ void load_delays(CoefPrefetch<NTS>& cp, const FusedAr
     cp.g[j] = 1.0f;
     if (P.gain) cp.g[j] = P.gain[m * P.A + a];  // uniform branch; absent gains cost nothing
   }
-}
-
-// Per-(a, m) real beam weight applied to the float32 phasor (one rounding per component, as the oracle).
-__device__ __forceinline__ void apply_gain(float g, float* re, float* im) {
-  *re = __fmul_rn(*re, g);
-  *im = __fmul_rn(*im, g);
 }
 
 template <bool Exact, int Mode, int NTS>
@@ -522,7 +503,6 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
 // i.e. half the MFMAs of the f16 hi/lo path and no byte->f16 conversion: each fragment dword is one v_perm of
 // two antennas' raw dwords.  k-slot (s, h, j) <-> antenna a = 32 s + 8 h + j/2, re/im = j & 1.  Unsigned samples
 // run as x - 128 (one xor) plus the exact correction 128 * sum_k W_k per column.
-inline int fused_kernel_choice();
 constexpr uint32_t kSelP0 = 0x05040100u;  // v_perm: [S1.b0, S1.b1, S0.b0, S0.b1]
 constexpr uint32_t kSelP1 = 0x07060302u;  // v_perm: [S1.b2, S1.b3, S0.b2, S0.b3]
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
@@ -1013,13 +993,14 @@ int launch_i8(FusedArgs P, hipStream_t st) {
 // ---------------------------------------------------------------------------------------------------------
 // Kernel choice for A <= 64, T <= 256: BF_FUSED_KERNEL = item (default) | pipe | generic; BF_FUSED_GENERIC=1 is
 // shorthand for generic (tests run every path against the oracle).
-inline int fused_kernel_choice() {
+int fused_kernel_choice() {
   const char* g = getenv("BF_FUSED_GENERIC");
   if (g && g[0] == '1') return 2;
   const char* e = getenv("BF_FUSED_KERNEL");
   if (!e) return 0;
   if (e[0] == 'p') return 1;
   if (e[0] == 'g') return 2;
+  if (e[0] == 'w') return 3;
   return 0;
 }
 
@@ -1072,6 +1053,11 @@ template <bool Signed, bool OutI8, bool Exact>
 int dispatch(FusedArgs P, hipStream_t st) {
   const int choice = fused_kernel_choice();
   const bool small = P.S <= kGroup && P.T <= 256;
+  if constexpr (!OutI8) {
+    // many antennas x beams (config 4): the wide kernel keeps every beam of the item in one workgroup
+    const bool wide = (choice == 3) || (choice == 0 && P.M >= 24 && (!small || P.M > 32));
+    if (wide && wide_fits(P)) return launch_wide<Signed, Exact>(P, st);
+  }
   if (small && choice != 2) {
     const int M2 = 2 * P.M;
     if (choice == 1) {

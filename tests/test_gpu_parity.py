@@ -252,10 +252,15 @@ def test_fused_equals_op_sequence_bitwise(context, command_queue, fused_path):
                           O.coeffs(d, B, 2, C, Ctot, A, M, 2))
 
 
-@pytest.fixture(params=["item", "pipe", "generic"])
+@pytest.fixture(params=["item", "pipe", "generic", "wide", "wide32"])
 def fused_path(request, monkeypatch):
     """Run a fused test through each kernel: the single-item kernel (default for A <= 64, T <= 256), the
-    persistent pipelined kernel, and the generic kernel (what larger shapes use)."""
+    persistent pipelined kernel, the generic kernel, and the wide kernel (default for many antennas x beams;
+    64- and 32-beam slabs).  int8 output has its own kernels and ignores 'wide'."""
+    if request.param == "wide32":
+        monkeypatch.setenv("BF_FUSED_WIDE_TW", "1")
+        monkeypatch.setenv("BF_FUSED_KERNEL", "wide")
+        return "wide"
     monkeypatch.delenv("BF_FUSED_GENERIC", raising=False)
     monkeypatch.setenv("BF_FUSED_KERNEL", request.param)
     return request.param

@@ -46,6 +46,21 @@ names = {0: "full (fast coef)", 128: "cached loads", 256: "nt stores", 384: "cac
          3: "no-coef,no-mfma", 5: "no-coef,no-store", 9: "no-coef,no-load", 7: "loads only", 11: "stores only"}
 print(f"shape B={B} C={C} T={T} A={A} M={M}: in {nin/2**30:.2f} GiB out {nout/2**30:.2f} GiB")
 ROUNDS = int(_os.environ.get("DIAG_ROUNDS", "1"))
+if "wide" in _os.environ.get("DIAG_KERNELS", ""):
+    lib.bf_diag_wide.argtypes = [I, I, V, V, V, I, I, I, I, I, I, D, V]
+    wnames = {0: "full (fast coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 3: "no-coef,no-mfma",
+              5: "no-coef,no-store"}
+    Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
+    for tw in (2, 1):
+        res = {m: [] for m in wnames}
+        for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
+            for mode in wnames:
+                res[mode].append(timeit(lambda i: lib.bf_diag_wide(mode, tw, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
+                                                                   B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
+        for mode in wnames:
+            ts = sorted(res[mode])
+            print(f"  wide tw={tw} mode {mode:2d} {wnames[mode]:18s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
+                  f"alg {alg / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
 names_i8 = {0: "full (exact coef)", 16: "fast coef", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store",
             5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
             65: "occ 2, no-store"}

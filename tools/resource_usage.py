@@ -1,8 +1,10 @@
-"""Print per-kernel VGPR/AGPR/SGPR/scratch/occupancy for a HIP source (hipcc -Rpass-analysis)."""
+"""Print per-kernel VGPR/AGPR/SGPR/scratch/occupancy for a HIP source (hipcc -Rpass-analysis).
+    python tools/resource_usage.py <file.hip> [extra hipcc flags ...]"""
 import re, subprocess, sys
 src = sys.argv[1]
 out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-x", "hip", "-c", src,
-                      "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
+                      "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage"] + sys.argv[2:],
+                     capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
     m = re.search(r"remark: (.*?) \[-Rpass", line)
@@ -17,5 +19,5 @@ for line in out.splitlines():
         cur[k.strip()] = v.strip()
 for r in rows:
     n = subprocess.run(["c++filt"], input=r["name"], capture_output=True, text=True).stdout.strip()
-    n = re.sub(r"\(.*", "", n)
+    n = re.sub(r"\(.*", "", n).replace("bf::(anonymous namespace)::", "")
     print(f"{n[:70]:70s} V={r.get('VGPRs')} A={r.get('AGPRs')} S={r.get('SGPRs')} scr={r.get('ScratchSize [bytes/lane]')} occ={r.get('Occupancy [waves/SIMD]')}")
