@@ -26,9 +26,52 @@
 //                             contiguous, so a 16-byte load = 4 samples x 2 pols of one antenna and the
 //                             reorder costs no HBM traffic), W generated in float64 in-kernel per (b, c) from
 //                             the delay model.  One workgroup per (b, c[, slab]), both pols.
+#include <cstdlib>
+
 #include "bf_mfma.hpp"
 
 namespace bf {
+
+// ---------------------------------------------------------------------------------------------------------
+// Stage W[b,p,c][:, slab columns] (rows k < Sp*32, zero past 2A and past 2M) -> hi/lo fragments in LDS.  Each thread
+// moves 4 consecutive columns of a row per float4 load (2M % 4 == 0; scalar otherwise), and batches of 8 loads are
+// all issued before their conversions: a load-then-convert loop paid one memory latency per element.
+template <int NTS>
+__device__ __forceinline__ void stage_table(_Float16* lh, const float* __restrict__ wp, int K2, int M2, int Sp,
+                                            int tau0, int nts, int tid) {
+  const int cols = nts * 16, c4 = cols >> 2;
+  const int n4 = Sp * 32 * c4;
+  const bool vec = (M2 & 3) == 0 && (reinterpret_cast<uintptr_t>(wp) & 15) == 0;  // 16-byte rows (uniform)
+  for (int base = 0; base < n4; base += 8 * kThreads) {
+    float4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = min(base + j * kThreads + tid, n4 - 1);
+      const int k = e / c4, cl = (e - k * c4) * 4;
+      const int col = tau0 * 16 + cl;
+      const int kk = min(k, K2 - 1);
+      if (vec) {
+        v[j] = *reinterpret_cast<const float4*>(wp + static_cast<size_t>(kk) * M2 + min(col, M2 - 4));
+      } else {
+        const float* r = wp + static_cast<size_t>(kk) * M2;
+        v[j] = float4{r[min(col, M2 - 1)], r[min(col + 1, M2 - 1)], r[min(col + 2, M2 - 1)], r[min(col + 3, M2 - 1)]};
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = base + j * kThreads + tid;
+      if (e >= n4) break;
+      const int k = e / c4, cl = (e - k * c4) * 4;
+      const int col = tau0 * 16 + cl;
+      const float vals[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float val = (k < K2 && col + q < M2) ? vals[q] : 0.0f;
+        put_split(lh, coef_elem(k, cl + q, nts), val);
+      }
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------------------------------------
 // MatrixMultiply drop-in.  grid = B*P*C*nslabs; a slab is NTS 16-column tiles of the 2M outputs.
@@ -46,19 +89,8 @@ __global__ __launch_bounds__(kThreads) void beamform_table_kernel(const uint8_t*
   const int nts = min(NTS, NT - tau0);
   const int K2 = 2 * A, M2 = 2 * M;
 
-  // Stage W[b,p,c][:, slab columns] -> hi/lo fragments (coalesced along the 2M row).
-  {
-    const float* wp = w + bpc * static_cast<size_t>(K2) * M2;
-    _Float16* lh = reinterpret_cast<_Float16*>(lds);
-    const int cols = nts * 16;
-    const int nel = S * 32 * cols;
-    for (int e = tid; e < nel; e += kThreads) {
-      const int k = e / cols, cl = e - k * cols;
-      const int col = tau0 * 16 + cl;
-      const float v = (k < K2 && col < M2) ? wp[static_cast<size_t>(k) * M2 + col] : 0.0f;
-      put_split(lh, coef_elem(k, cl, nts), v);
-    }
-  }
+  stage_table<NTS>(reinterpret_cast<_Float16*>(lds), w + bpc * static_cast<size_t>(K2) * M2, K2, M2, S, tau0, nts,
+                   tid);
   __syncthreads();
 
   const int T = NB * kSamplesPerBlock;
@@ -113,6 +145,80 @@ __global__ __launch_bounds__(kThreads) void beamform_table_kernel(const uint8_t*
   }
 }
 
+// Streaming variant for A % 4 == 0 (8-byte fragment loads): a wave's k-step fragments of all its row groups form one
+// stream that runs through a register ring of R uint2, refilled R steps ahead by unconditional loads (address clamped
+// inside the table; steps past S meet zero coefficients).  The loop body is identical every iteration, so the
+// compiler's vmcnt waits stay exact (vmcnt(R-1) per step) and R loads stay in flight -- the per-step load-then-use of
+// the basic kernel paid one memory latency per k-step (32 per row at 256 antennas).
+template <bool Signed, int NTS, int R>
+__global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uint8_t* __restrict__ x,
+                                                                       const float* __restrict__ w,
+                                                                       float* __restrict__ y, int NB, int A, int M,
+                                                                       int S, int NT, int nslabs) {
+  extern __shared__ __attribute__((aligned(16))) half8 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int slab = blockIdx.x % nslabs;
+  const size_t bpc = blockIdx.x / nslabs;
+  const int tau0 = slab * NTS;
+  const int nts = min(NTS, NT - tau0);
+  const int K2 = 2 * A, M2 = 2 * M;
+  const int Sp = (S + R - 1) / R * R;  // padded steps per row group
+
+  stage_table<NTS>(reinterpret_cast<_Float16*>(lds), w + bpc * static_cast<size_t>(K2) * M2, K2, M2, Sp, tau0, nts,
+                   tid);  // padded steps zero
+  __syncthreads();
+
+  const int T = NB * kSamplesPerBlock;
+  const uint8_t* xp = x + bpc * static_cast<size_t>(T) * K2;
+  float* yp = y + bpc * static_cast<size_t>(T) * M2;
+  const int h = lane >> 4, tl = lane & 15;
+  const int nrg = (NB - wave + kWaves - 1) / kWaves;  // this wave's row groups (rg = wave + 4 j)
+  if (nrg <= 0) return;
+  const int nsteps = nrg * Sp;  // the wave's whole fragment stream
+  // stream position q -> (row group j = q / Sp, step s = q % Sp); byte offset of the lane's 8 bytes, clamped
+  auto src = [&](int q) -> const uint2* {
+    q = min(q, nsteps - 1);
+    const int j = q / Sp, s = q - j * Sp;
+    const int tt = (wave + kWaves * j) * kSamplesPerBlock + tl;
+    const int k0 = min(32 * s + 8 * h, K2 - 8);
+    return reinterpret_cast<const uint2*>(xp + static_cast<size_t>(tt) * K2 + k0);
+  };
+  uint2 ring[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) ring[r] = *src(r);
+
+  f32x4 acc[NTS];
+#pragma unroll
+  for (int tau = 0; tau < NTS; ++tau) acc[tau] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q0 = 0; q0 < nsteps; q0 += R) {
+    const int j = q0 / Sp, s0 = q0 - j * Sp;  // R divides Sp: a ring turn stays inside one row group
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint2 cur = ring[r];
+      ring[r] = *src(q0 + R + r);
+      const int s = s0 + r;
+      const half8 v = bytes8_to_frag<Signed>(cur.x, cur.y);
+#pragma unroll
+      for (int tau = 0; tau < NTS; ++tau) {
+        if (tau < nts) {
+          const int slot = ((s * nts + tau) * 2) * 64;
+          acc[tau] = mfma(lds[slot + lane], v, acc[tau]);
+          acc[tau] = mfma(lds[slot + 64 + lane], v, acc[tau]);
+        }
+      }
+    }
+    if (s0 + R == Sp) {  // row group j complete: store and restart the accumulators
+      const int tt = (wave + kWaves * j) * kSamplesPerBlock + tl;
+      float* orow = yp + static_cast<size_t>(tt) * M2;
+#pragma unroll
+      for (int tau = 0; tau < NTS; ++tau) {
+        if (tau < nts) store_f32<NTS>(orow, 16 * (tau0 + tau) + 4 * h, M2, acc[tau]);
+        acc[tau] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+}
+
 template <bool Signed, int NTS, bool Vec8>
 int launch_table(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                  hipStream_t st) {
@@ -126,9 +232,32 @@ int launch_table(const uint8_t* x, const float* w, float* y, long long bpc, int 
   BF_LAUNCHED("beamform_table_kernel");
 }
 
+template <bool Signed, int NTS, int R>
+int launch_ring(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
+                hipStream_t st) {
+  const int nslabs = (NT + NTS - 1) / NTS;
+  const int Sp = (S + R - 1) / R * R;
+  const size_t lds = coef_lds_bytes(Sp, NTS);
+  BF_REQUIRE(lds <= kMaxLds, "bf_beamform: n_ants=%d too large for one coefficient slab", A);
+  const long long grid = bpc * nslabs;
+  BF_REQUIRE(grid < (1LL << 31), "bf_beamform: grid too large");
+  hipLaunchKernelGGL((beamform_table_ring_kernel<Signed, NTS, R>), dim3(static_cast<unsigned>(grid)), dim3(kThreads),
+                     lds, st, x, w, y, NB, A, M, S, NT, nslabs);
+  BF_LAUNCHED("beamform_table_ring_kernel");
+}
+
 template <bool Signed, int NTS>
 int dispatch_vec(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                  hipStream_t st) {
+  const char* e = getenv("BF_TABLE_BASIC");  // tests: force the basic kernel
+  if (A % 4 == 0 && !(e && e[0] == '1')) {
+    // ring depth: the k-steps of a row, up to 16 (the steps are padded to a multiple of R); long rows only
+    if (S >= 16 && coef_lds_bytes((S + 15) / 16 * 16, NTS) <= kMaxLds)
+      return launch_ring<Signed, NTS, 16>(x, w, y, bpc, NB, A, M, S, NT, st);
+    if (S >= 8 && coef_lds_bytes((S + 7) / 8 * 8, NTS) <= kMaxLds)
+      return launch_ring<Signed, NTS, 8>(x, w, y, bpc, NB, A, M, S, NT, st);
+    // (below 8 k-steps the basic kernel's small LDS footprint keeps enough workgroups resident to hide latency)
+  }
   if (A % 4 == 0) return launch_table<Signed, NTS, true>(x, w, y, bpc, NB, A, M, S, NT, st);
   return launch_table<Signed, NTS, false>(x, w, y, bpc, NB, A, M, S, NT, st);
 }

@@ -6,11 +6,15 @@
 // (b, c, time-chunk) tile: every antenna's contiguous run of TT*4 bytes is loaded with 16-byte coalesced
 // loads into an LDS image [A][TT*4 (+4 pad)], and the output -- which for a fixed (b, p, c) and time chunk
 // is ONE contiguous run of TT*A u16 -- is written with 16-byte coalesced stores (8 antennas per lane).
-// The odd dword pitch (TT + 1) keeps the 2-byte transposed LDS reads bank-conflict-free.
+// Loads are issued in batches of 8 per thread before their LDS writes (a load-then-write loop paid one HBM latency
+// per iteration).  For A % 8 == 0 a thread reads the 8 antennas' dwords of one time sample (both pols) and splits
+// them with v_perm into the two pols' outputs; other A use 2-byte transposed reads.  The odd dword pitch (TT + 1)
+// keeps the transposed LDS reads (nearly) bank-conflict-free.
 #include "bf_common.hpp"
 
 namespace bf {
 
+template <bool Oct>
 __global__ __launch_bounds__(256) void reorder_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                       int A, int C, int T, int TT, int nchunk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_u32[];
@@ -21,44 +25,89 @@ __global__ __launch_bounds__(256) void reorder_kernel(const uint8_t* __restrict_
   const int t0 = chunk * TT;
   const int pitch = TT + 1;  // dwords per antenna row
   const int quads = TT >> 2;
+  const int nq = A * quads;
 
-  // 1. antenna runs -> LDS.  in[b][a][c][t][p][ri], one 16-byte load = 4 time samples x 2 pols x (re, im).
-  for (int idx = threadIdx.x; idx < A * quads; idx += blockDim.x) {
-    const int a = idx / quads;
-    const int tq = idx - a * quads;
-    const size_t src = ((static_cast<size_t>(b) * A + a) * C + c) * static_cast<size_t>(T) * 4 +
-                       static_cast<size_t>(t0 + 4 * tq) * 4;
-    const uint4 v = *reinterpret_cast<const uint4*>(in + src);
-    uint32_t* row = lds_u32 + a * pitch + 4 * tq;
-    row[0] = v.x;
-    row[1] = v.y;
-    row[2] = v.z;
-    row[3] = v.w;
+  // 1. antenna runs -> LDS.  in[b][a][c][t][p][ri], one 16-byte load = 4 time samples x 2 pols x (re, im).  Batches
+  // of 8 loads per thread are all issued (unconditional, clamped) before their LDS writes.
+  for (int base = 0; base < nq; base += 8 * 256) {
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = min(base + k * 256 + static_cast<int>(threadIdx.x), nq - 1);
+      const int a = idx / quads;
+      const int tq = idx - a * quads;
+      const size_t src = ((static_cast<size_t>(b) * A + a) * C + c) * static_cast<size_t>(T) * 4 +
+                         static_cast<size_t>(t0 + 4 * tq) * 4;
+      v[k] = *reinterpret_cast<const uint4*>(in + src);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = base + k * 256 + static_cast<int>(threadIdx.x);
+      if (idx < nq) {
+        const int a = idx / quads;
+        const int tq = idx - a * quads;
+        uint32_t* row = lds_u32 + a * pitch + 4 * tq;
+        row[0] = v[k].x;
+        row[1] = v[k].y;
+        row[2] = v[k].z;
+        row[3] = v[k].w;
+      }
+    }
   }
   __syncthreads();
 
   // 2. LDS -> out[b][p][c][t][a][ri]: for each pol the chunk is TT*A contiguous u16 (16-byte aligned).
-  const uint16_t* lds_u16 = reinterpret_cast<const uint16_t*>(lds_u32);
-  const int n_u16 = TT * A;
-  for (int p = 0; p < 2; ++p) {
-    uint8_t* dst = out + ((static_cast<size_t>(b) * 2 + p) * C + c) * static_cast<size_t>(T) * A * 2 +
-                   static_cast<size_t>(t0) * A * 2;
-    for (int e0 = threadIdx.x * 8; e0 < n_u16; e0 += blockDim.x * 8) {
-      uint32_t w[4];
+  uint8_t* dst0 = out + ((static_cast<size_t>(b) * 2 + 0) * C + c) * static_cast<size_t>(T) * A * 2 +
+                  static_cast<size_t>(t0) * A * 2;
+  uint8_t* dst1 = out + ((static_cast<size_t>(b) * 2 + 1) * C + c) * static_cast<size_t>(T) * A * 2 +
+                  static_cast<size_t>(t0) * A * 2;
+  if constexpr (Oct) {
+    // A % 8 == 0: a thread owns (t, 8 antennas a0..a0+7): 8 dword reads give both pols' (re, im) of the 8 antennas
+    // and one v_perm per output dword splits them into the pol-0 and pol-1 16-byte outputs (antenna group fastest
+    // across lanes, so the stores are contiguous; the odd row pitch keeps the reads at most 2-way conflicted)
+    const int ngrp = A >> 3;
+    const int n_items = TT * ngrp;
+    for (int it = threadIdx.x; it < n_items; it += 256) {
+      const int t = it / ngrp;
+      const int a0 = (it - t * ngrp) * 8;
+      uint32_t d[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t pair = 0;
+      for (int j = 0; j < 8; ++j) d[j] = lds_u32[(a0 + j) * pitch + t];
+      uint4 w0, w1;  // pol 0: low halves (u16 0) of each antenna's dword; pol 1: high halves
+      w0.x = __builtin_amdgcn_perm(d[1], d[0], 0x05040100u);
+      w0.y = __builtin_amdgcn_perm(d[3], d[2], 0x05040100u);
+      w0.z = __builtin_amdgcn_perm(d[5], d[4], 0x05040100u);
+      w0.w = __builtin_amdgcn_perm(d[7], d[6], 0x05040100u);
+      w1.x = __builtin_amdgcn_perm(d[1], d[0], 0x07060302u);
+      w1.y = __builtin_amdgcn_perm(d[3], d[2], 0x07060302u);
+      w1.z = __builtin_amdgcn_perm(d[5], d[4], 0x07060302u);
+      w1.w = __builtin_amdgcn_perm(d[7], d[6], 0x07060302u);
+      const size_t off = (static_cast<size_t>(t) * A + a0) * 2;
+      *reinterpret_cast<uint4*>(dst0 + off) = w0;
+      *reinterpret_cast<uint4*>(dst1 + off) = w1;
+    }
+  } else {
+    const uint16_t* lds_u16 = reinterpret_cast<const uint16_t*>(lds_u32);
+    const int n_u16 = TT * A;
+    for (int p = 0; p < 2; ++p) {
+      uint8_t* dst = p ? dst1 : dst0;
+      for (int e0 = threadIdx.x * 8; e0 < n_u16; e0 += blockDim.x * 8) {
+        uint32_t w[4];
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const int e = e0 + 2 * j + half;
-          const int t = e / A;
-          const int a = e - t * A;
-          // element (a, t, p) of the LDS image, in u16 units: a*pitch*2 + t*2 + p
-          pair |= static_cast<uint32_t>(lds_u16[a * pitch * 2 + t * 2 + p]) << (16 * half);
+        for (int j = 0; j < 4; ++j) {
+          uint32_t pair = 0;
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int e = e0 + 2 * j + half;
+            const int t = e / A;
+            const int a = e - t * A;
+            // element (a, t, p) of the LDS image, in u16 units: a*pitch*2 + t*2 + p
+            pair |= static_cast<uint32_t>(lds_u16[a * pitch * 2 + t * 2 + p]) << (16 * half);
+          }
+          w[j] = pair;
         }
-        w[j] = pair;
+        *reinterpret_cast<uint4*>(dst + static_cast<size_t>(e0) * 2) = make_uint4(w[0], w[1], w[2], w[3]);
       }
-      *reinterpret_cast<uint4*>(dst + static_cast<size_t>(e0) * 2) = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
 }
@@ -81,7 +130,12 @@ extern "C" int bf_reorder(const uint8_t* in, uint8_t* out, int B, int A, int C, 
   const long long grid = static_cast<long long>(B) * C * nchunk;
   BF_REQUIRE(grid < (1LL << 31), "bf_reorder: grid too large");
   const size_t lds = static_cast<size_t>(A) * (TT + 1) * 4;
-  hipLaunchKernelGGL(bf::reorder_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), lds, bf::as_stream(stream),
-                     in, out, A, C, T, TT, nchunk);
+  if (A % 8 == 0) {
+    hipLaunchKernelGGL(bf::reorder_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(256), lds,
+                       bf::as_stream(stream), in, out, A, C, T, TT, nchunk);
+  } else {
+    hipLaunchKernelGGL(bf::reorder_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(256), lds,
+                       bf::as_stream(stream), in, out, A, C, T, TT, nchunk);
+  }
   BF_LAUNCHED("reorder_kernel");
 }
