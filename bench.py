@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
     p.add_argument("--out-int8", action="store_true", help="int8 requantised beams instead of float32")
+    p.add_argument("--unsigned", action="store_true", help="uint8 voltages (the reference slots' dtype) instead of int8")
     p.add_argument("--nbuf", type=int, default=2, help="rotating input/output buffer sets (defeat the 256 MB MALL)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
@@ -99,7 +100,9 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def make_inputs(np, rng, shape, nbuf):
+def make_inputs(np, rng, shape, nbuf, unsigned=False):
+    if unsigned:
+        return [rng.integers(0, 256, size=shape, dtype=np.uint8) for _ in range(nbuf)]
     return [rng.integers(-128, 128, size=shape, dtype=np.int8) for _ in range(nbuf)]
 
 
@@ -117,7 +120,7 @@ def run_gpu(args, dist, wl):
     A, M, C, T, B = wl["A"], wl["M"], wl["C"], wl["T"], wl["B"]
     Ctot = wl.get("Ctot", C * max(dist.world, 1))
     tmpl = FusedBeamformerTemplate(ctx, B, C, Ctot, T, A, M, xeng_id=dist.rank, sample_period=TS, delay_channels=1,
-                                   sample_signed=True, out_int8=args.out_int8, out_scale=1 / 64,
+                                   sample_signed=not args.unsigned, out_int8=args.out_int8, out_scale=1 / 64,
                                    t0=0.0, batch_dt=T * 2 * Ctot * TS)
     rng = np.random.default_rng(1 + dist.rank)
     d = np.zeros(tmpl.delay_shape, np.float32)  # compact (1, M, A, 4) polynomial delay model with rates
@@ -126,7 +129,7 @@ def run_gpu(args, dist, wl):
     d[..., 2] = rng.uniform(-np.pi, np.pi, d.shape[:-1])
     d[..., 3] = rng.uniform(-1, 1, d.shape[:-1])
     ops = []
-    for i, host in enumerate(make_inputs(np, rng, tmpl.input_shape, args.nbuf)):
+    for i, host in enumerate(make_inputs(np, rng, tmpl.input_shape, args.nbuf, args.unsigned)):
         op = tmpl.instantiate(queue)
         op.ensure_all_bound()
         op.buffer("inSamples").set(queue, host)
@@ -202,7 +205,8 @@ def pmc_traffic(args):
         out = tempfile.mkdtemp(prefix="bfpmc_", dir=os.environ.get("TMPDIR", "/tmp"))
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
-               "--steps", "3", "--warmup", "1"] + (["--out-int8"] if args.out_int8 else [])
+               "--steps", "3", "--warmup", "1"] + (["--out-int8"] if args.out_int8 else []) + \
+              (["--unsigned"] if args.unsigned else [])
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
         if r.returncode != 0 or not files:
@@ -260,7 +264,7 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "Gsamples/s", "n_gpus": dist.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["t_max"] / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
-        "data": "synthetic (uniform random int8 voltages, random delay/phase polynomials)",
+        "data": "synthetic (uniform random %s voltages, random delay/phase polynomials)" % ("uint8" if args.unsigned else "int8"),
         "config": {"workload": args.workload + ": " + wl["desc"], "n_ants": wl["A"], "n_beams": wl["M"],
                    "n_channels_per_gpu": wl["C"], "n_samples_per_channel": wl["T"], "n_batches": wl["B"],
                    "n_pols": 2, "output": "int8" if args.out_int8 else "float32",
