@@ -17,26 +17,26 @@
 
 namespace bf {
 
+// One thread per (c, a, m): grid (ceil(A*M / 256), C), 32-bit index math (the grid-stride form with 64-bit
+// divisions spent more time on index arithmetic and serial load latency than on the phasor or the writes).
 __global__ __launch_bounds__(256) void coeff_gen_kernel(const float4* __restrict__ dv, float* __restrict__ out,
                                                         int B, int P, int C, int A, int M, long long base_ch,
                                                         double ctot, double ts) {
-  const long long n = static_cast<long long>(C) * A * M;
-  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+  const int am = static_cast<int>(blockIdx.x) * 256 + static_cast<int>(threadIdx.x);
+  if (am >= A * M) return;
+  const int c = static_cast<int>(blockIdx.y);
+  const int a = am / M, m = am - a * M;
+  const float4 d = dv[(static_cast<size_t>(c) * M + m) * A + a];  // delay_vals[c][m][a]
+  float re, im;
+  steering_coeff(d, static_cast<double>(base_ch + c), make_phase(ctot, ts), 0.0, &re, &im);
+  const float2 row0 = make_float2(re, im);   // W[2a][2m], W[2a][2m+1]
+  const float2 row1 = make_float2(-im, re);  // W[2a+1][2m], W[2a+1][2m+1]
   const size_t plane = static_cast<size_t>(2 * A) * (2 * M);  // one (b, p, c) coefficient matrix
-  for (long long idx = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < n; idx += stride) {
-    const int m = static_cast<int>(idx % M);
-    const int a = static_cast<int>((idx / M) % A);
-    const int c = static_cast<int>(idx / (static_cast<long long>(M) * A));
-    const float4 d = dv[(static_cast<size_t>(c) * M + m) * A + a];  // delay_vals[c][m][a]
-    float re, im;
-    steering_coeff(d, static_cast<double>(base_ch + c), make_phase(ctot, ts), 0.0, &re, &im);
-    const float2 row0 = make_float2(re, im);   // W[2a][2m], W[2a][2m+1]
-    const float2 row1 = make_float2(-im, re);  // W[2a+1][2m], W[2a+1][2m+1]
-    for (int bp = 0; bp < B * P; ++bp) {
-      float* w = out + (static_cast<size_t>(bp) * C + c) * plane;
-      *reinterpret_cast<float2*>(w + static_cast<size_t>(2 * a) * (2 * M) + 2 * m) = row0;
-      *reinterpret_cast<float2*>(w + static_cast<size_t>(2 * a + 1) * (2 * M) + 2 * m) = row1;
-    }
+  float* w = out + static_cast<size_t>(c) * plane + static_cast<size_t>(2 * a) * (2 * M) + 2 * m;
+  const size_t bp_stride = static_cast<size_t>(C) * plane;
+  for (int bp = 0; bp < B * P; ++bp) {
+    *reinterpret_cast<float2*>(w + bp * bp_stride) = row0;
+    *reinterpret_cast<float2*>(w + bp * bp_stride + 2 * M) = row1;
   }
 }
 
@@ -82,8 +82,9 @@ extern "C" int bf_coeff_gen(const float* delay_vals, float* out, int B, int P, i
   BF_REQUIRE(sample_period > 0.0, "bf_coeff_gen: sample_period must be > 0");
   BF_REQUIRE((reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0,
              "bf_coeff_gen: misaligned buffer");
-  const long long n = static_cast<long long>(C) * A * M;
-  hipLaunchKernelGGL(bf::coeff_gen_kernel, dim3(bf::grid_for(n)), dim3(256), 0, bf::as_stream(stream),
+  BF_REQUIRE(static_cast<long long>(A) * M < (1LL << 31) && C < 65536, "bf_coeff_gen: shape too large");
+  const unsigned gx = static_cast<unsigned>((static_cast<long long>(A) * M + 255) / 256);
+  hipLaunchKernelGGL(bf::coeff_gen_kernel, dim3(gx, static_cast<unsigned>(C)), dim3(256), 0, bf::as_stream(stream),
                      reinterpret_cast<const float4*>(delay_vals), out, B, P, C, A, M,
                      static_cast<long long>(C) * xeng_id, static_cast<double>(Ctot), sample_period);
   BF_LAUNCHED("coeff_gen_kernel");
