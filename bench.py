@@ -234,7 +234,7 @@ def kernel_name(wl, out_int8):
     kernel (f32 beams) / the generic integer kernel (int8 beams)."""
     if wl["A"] <= 64 and wl["T"] <= 256:
         return KERNELS[out_int8][0]
-    return "beamform_fused_i8_kernel" if out_int8 else "beamform_fused_wide_kernel"
+    return "beamform_fused_i8_wide_kernel" if out_int8 else "beamform_fused_wide_kernel"
 
 
 def secondary(args, dist, workload, out_int8):
@@ -281,7 +281,8 @@ def main():
     del ops_queue
     if dist.rank == 0 and dist.world == 1 and not args.no_secondary and args.workload == "cfg3":
         line["secondary"] = []
-        for workload, out_int8 in (("cfg2", args.out_int8), ("cfg3", not args.out_int8), ("cfg4", args.out_int8)):
+        for workload, out_int8 in (("cfg2", args.out_int8), ("cfg3", not args.out_int8), ("cfg4", args.out_int8),
+                                   ("cfg4", not args.out_int8)):
             try:
                 line["secondary"].append(secondary(args, dist, workload, out_int8))
             except Exception as e:  # secondary lines are informational

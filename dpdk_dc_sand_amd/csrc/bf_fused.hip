@@ -503,19 +503,8 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
 // i.e. half the MFMAs of the f16 hi/lo path and no byte->f16 conversion: each fragment dword is one v_perm of
 // two antennas' raw dwords.  k-slot (s, h, j) <-> antenna a = 32 s + 8 h + j/2, re/im = j & 1.  Unsigned samples
 // run as x - 128 (one xor) plus the exact correction 128 * sum_k W_k per column.
-constexpr uint32_t kSelP0 = 0x05040100u;  // v_perm: [S1.b0, S1.b1, S0.b0, S0.b1]
-constexpr uint32_t kSelP1 = 0x07060302u;  // v_perm: [S1.b2, S1.b3, S0.b2, S0.b3]
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ i32x4_t mfma_i8(i32x4_t a, i32x4_t b, i32x4_t c) {
-  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
-}
 
-// LDS image: [s][tau][limb][lane] x 16 bytes, then 16*NTS int32 column sums.
-__device__ __forceinline__ int coef8_byte(int k, int cl, int nts, int limb) {
-  const int s = k >> 6, h = (k >> 4) & 3, j = k & 15, tau = cl >> 4, row = cl & 15;
-  return ((((s * nts + tau) * 2 + limb) * 64) + row + 16 * h) * 16 + j;
-}
 
 __device__ __forceinline__ void put_q14(int8_t* lb, int* colsum, int k, int cl, int nts, float w) {
   const int W = static_cast<int>(__builtin_rintf(w * 16384.0f));  // exact product, RNE
@@ -687,18 +676,6 @@ __device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* cols
   return packed;
 }
 
-// 4x4 transpose over (lane group h = lane >> 4, register i): afterwards lane group h holds v[i] = old v[h] of lane
-// group i.  Two stages of 2x2 block swaps (rows {0,1}<->{2,3}, then odd<->even rows); all 64 lanes must be active.
-__device__ __forceinline__ void transpose_rows4(uint32_t (&v)[4]) {
-  auto a = __builtin_amdgcn_permlane32_swap(v[0], v[2], false, false);
-  auto b = __builtin_amdgcn_permlane32_swap(v[1], v[3], false, false);
-  auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
-  auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
-  v[0] = c[0];
-  v[1] = c[1];
-  v[2] = d[0];
-  v[3] = d[1];
-}
 
 // Item form of the integer kernel (A <= 64, T <= 256): one (slab, b, c) per workgroup, issue order delay model ->
 // voltages (16 x 16 B per lane) -> exact coefficients + Q14 limbs under them -> barrier -> per pol: v_perm
@@ -963,7 +940,10 @@ int launch_i8_item(FusedArgs P, hipStream_t st, size_t min_lds = 0) {
 template <bool Signed>
 int launch_i8(FusedArgs P, hipStream_t st) {
   const int S8 = (2 * P.A + 63) / 64;
-  if (S8 <= 2 && P.T <= 256 && fused_kernel_choice() != 2) {
+  const int choice = fused_kernel_choice();
+  const bool small = S8 <= 2 && P.T <= 256;
+  if ((choice == 3 || (choice == 0 && !small)) && i8_wide_fits(P)) return launch_i8_wide<Signed>(P, st);
+  if (small && choice != 2) {
     const int M2 = 2 * P.M;
     if (P.NT >= 2) {
       if (M2 % 32 == 0) return launch_i8_item<Signed, 2, true>(P, st);

@@ -26,8 +26,42 @@ __device__ __forceinline__ void apply_gain(float g, float* re, float* im) {
   *im = __fmul_rn(*im, g);
 }
 
+
+// ---- integer (int8-output) path helpers: v_mfma_i32_16x16x64_i8 fragments, Q14 limb LDS image, row transpose
+constexpr uint32_t kSelP0 = 0x05040100u;  // v_perm: [S1.b0, S1.b1, S0.b0, S0.b1]
+constexpr uint32_t kSelP1 = 0x07060302u;  // v_perm: [S1.b2, S1.b3, S0.b2, S0.b3]
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4_t mfma_i8(i32x4_t a, i32x4_t b, i32x4_t c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+// LDS image: [s][tau][limb][lane] x 16 bytes, then 16*NTS int32 column sums.
+__device__ __forceinline__ int coef8_byte(int k, int cl, int nts, int limb) {
+  const int s = k >> 6, h = (k >> 4) & 3, j = k & 15, tau = cl >> 4, row = cl & 15;
+  return ((((s * nts + tau) * 2 + limb) * 64) + row + 16 * h) * 16 + j;
+}
+
+// 4x4 transpose over (lane group h = lane >> 4, register i): afterwards lane group h holds v[i] = old v[h] of lane
+// group i.  Two stages of 2x2 block swaps (rows {0,1}<->{2,3}, then odd<->even rows); all 64 lanes must be active.
+__device__ __forceinline__ void transpose_rows4(uint32_t (&v)[4]) {
+  auto a = __builtin_amdgcn_permlane32_swap(v[0], v[2], false, false);
+  auto b = __builtin_amdgcn_permlane32_swap(v[1], v[3], false, false);
+  auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+  auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+  v[0] = c[0];
+  v[1] = c[1];
+  v[2] = d[0];
+  v[3] = d[1];
+}
+
 // BF_FUSED_KERNEL = item (default) | pipe | generic | wide; BF_FUSED_GENERIC=1 is shorthand for generic.
 int fused_kernel_choice();
+
+// Integer wide kernel (bf_wide_i8.hip): int8 beams for many antennas x beams.
+bool i8_wide_fits(const FusedArgs& P);
+template <bool Signed>
+int launch_i8_wide(FusedArgs P, hipStream_t st);
 
 // Wide kernel (bf_wide.hip): returns BF_ERR_ARG without launching when the shape does not fit it.
 bool wide_fits(const FusedArgs& P);

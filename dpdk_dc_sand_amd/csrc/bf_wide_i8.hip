@@ -1,0 +1,356 @@
+// Integer wide fused beamformer: many antennas x beams (config 4: 256 antennas, 64 beams), int8 beams, bit-exact.
+//
+// Same integer contract as beamform_fused_i8_item_kernel (oracle.fused_beamform_int8: Q14 coefficients of the
+// exact float32 phasors, exact int32 products, one float rounding to int8), organised like the float wide kernel
+// (bf_wide.hip) for a per-item GEMM too large for the item kernel: workgroup = 4 waves x (64 samples, 16 beams,
+// both pols) per (b, c, 16-beam slab); the four slabs of a 64-beam item are XCD-ordered, so slabs after the first
+// re-read the voltages from L2.  The full [[R, I], [-I, R]] Q14 table (the float kernel's [R, -I] + [x_im, -x_re]
+// trick would need -x_re, which overflows int8 at -128) of a 16-beam slab is 2A x 32 x 2 limbs = 32 KiB at A = 256.
+// Per k-step (64 k = 32 antennas) a lane loads 8 antennas' 16-byte runs (uniform base + 32-bit lane offset; the last
+// step is pulled back to [A - 32, A) with zero rows for antennas already covered) and builds each pol's fragment
+// with one v_perm per dword; hi and lo limbs accumulate in separate int32 registers, combined once at the end as
+// (hi << 8) + lo (the item kernel's per-step fold would cost 8 VALU per tile per step here).
+#include <algorithm>
+#include <cstdlib>
+
+#include "bf_fused.hpp"
+
+namespace bf {
+
+namespace {
+
+constexpr int kW8Threads = 256;
+constexpr int kW8Beams = 16;  // beams per workgroup slab (2 tiles of 16 real columns)
+
+__device__ __forceinline__ int w8_step_base(int s, int A) { return min(32 * s, A - 32); }
+// k-steps of 32 antennas, padded to an even count (ping-pong, see the float wide kernel)
+__host__ __device__ inline int w8_padded_steps(int A) { return 2 * ((((A + 31) >> 5) + 1) / 2); }
+
+template <int Mode>
+__device__ __forceinline__ void w8_load(const uint8_t* __restrict__ base, size_t ant_stride, uint32_t loff, int s,
+                                        int A, uint32_t (&d)[8][4]) {
+  const int a0 = w8_step_base(s, A);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if constexpr (Mode & 8) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[q][j] = loff * 0x01010101u + s + q + j;
+      continue;
+    }
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a0 + q) * ant_stride + loff);
+    d[q][0] = v[0];
+    d[q][1] = v[1];
+    d[q][2] = v[2];
+    d[q][3] = v[3];
+  }
+}
+
+template <bool Signed, int Mode>
+__device__ __forceinline__ void w8_contract(const int4* __restrict__ fr, int s, int lane, const uint32_t (&d)[8][4],
+                                            i32x4_t (&hi)[2][4][2], i32x4_t (&lo)[2][4][2]) {
+  i32x4_t chi[2], clo[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int4 x0 = fr[(((s * 2 + t) * 2 + 0) * 64) + lane];
+    const int4 x1 = fr[(((s * 2 + t) * 2 + 1) * 64) + lane];
+    chi[t] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
+    clo[t] = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const uint32_t sel = p ? kSelP1 : kSelP0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t w[4];
+#pragma unroll
+      for (int m2 = 0; m2 < 4; ++m2) {
+        uint32_t a = d[2 * m2][i], b = d[2 * m2 + 1][i];
+        if constexpr (!Signed) {  // x - 128 as int8 (128 * column sum added back at the end)
+          a ^= 0x80808080u;
+          b ^= 0x80808080u;
+        }
+        w[m2] = __builtin_amdgcn_perm(b, a, sel);
+      }
+      const i32x4_t f = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]),
+                                static_cast<int>(w[3])};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if constexpr (Mode & 2) {
+          hi[p][i][t] += f + chi[t];
+          lo[p][i][t] += f + clo[t];
+        } else {
+          hi[p][i][t] = mfma_i8(chi[t], f, hi[p][i][t]);
+          lo[p][i][t] = mfma_i8(clo[t], f, lo[p][i][t]);
+        }
+      }
+    }
+  }
+}
+
+// Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads.
+template <bool Signed, int Mode = 0>
+__global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(FusedArgs P) {
+  extern __shared__ __attribute__((aligned(16))) int4 lds4[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  int slab, bc;
+  if (P.xcd_order) {  // the slabs of one item back to back on one XCD: later slabs re-read the voltages from L2
+    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
+    slab = local % P.nslabs;
+    bc = (local / P.nslabs) * 8 + x;
+    if (bc >= P.B * P.C) return;
+  } else {
+    slab = blockIdx.x % P.nslabs;
+    bc = blockIdx.x / P.nslabs;
+  }
+  const int b = bc / P.C, c = bc % P.C;
+  const int m0 = slab * kW8Beams;
+  const int Sp = w8_padded_steps(P.A);
+  const int T4 = P.T >> 2;
+  const int npasses = (((T4 + 15) >> 4) + 3) >> 2;  // 64-sample chunks per wave, the same count for every wave
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  const uint32_t hoff = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride);  // < 24 * stride
+  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+  int8_t* lb = reinterpret_cast<int8_t*>(lds4);
+  int* partial = reinterpret_cast<int*>(lb + static_cast<size_t>(Sp) * 2 * 2 * 64 * 16);  // [4 waves][32 columns]
+
+  uint32_t d0[8][4], d1[8][4];
+  int chunk = wave;
+  uint32_t loff = hoff + static_cast<uint32_t>(min(chunk * 16 + tl, T4 - 1)) * 16u;
+  w8_load<Mode>(base, ant_stride, loff, 0, P.A, d0);
+  w8_load<Mode>(base, ant_stride, loff, 1, P.A, d1);
+
+  // Q14 limbs of the slab's [[R, I], [-I, R]] blocks for every slot antenna (exact float64 phasors), under the
+  // loads.  Pair e -> 4 consecutive slot antennas x beam row ml (ml is fixed per thread: the column sums of the
+  // unsigned correction reduce over the 4 lanes sharing it).
+  {
+    const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+    const double ch = static_cast<double>(P.base_ch + c);
+    const int cd = P.delay_channels == 1 ? 0 : c;
+    const int npairs = 32 * Sp * kW8Beams;
+    int cs0 = 0, cs1 = 0;
+    constexpr int kBatch = 8;
+    for (int e0 = tid; e0 < npairs; e0 += kBatch * kW8Threads) {
+      float4 dv[kBatch];
+      float gv[kBatch];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        if constexpr (Mode & 1) break;
+        const int e = e0 + j * kW8Threads;
+        const int sa = 4 * ((e >> 2) / kW8Beams) + (e & 3);
+        const int a = min(w8_step_base(sa >> 5, P.A) + (sa & 31), P.A - 1);
+        const int m = min(m0 + (e >> 2) % kW8Beams, P.M - 1);
+        dv[j] = P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a];
+        gv[j] = 1.0f;
+        if (P.gain) gv[j] = P.gain[m * P.A + a];
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int e = e0 + j * kW8Threads;
+        if (e >= npairs) break;
+        const int ml = (e >> 2) % kW8Beams;
+        const int sa = 4 * ((e >> 2) / kW8Beams) + (e & 3);
+        const int a = w8_step_base(sa >> 5, P.A) + (sa & 31);
+        const int m = m0 + ml;
+        float re = 0.0f, im = 0.0f;
+        if constexpr (Mode & 1) {
+          re = 0.5f + 1e-3f * a;
+          im = 0.25f - 1e-3f * m;
+        } else if (a >= 32 * (sa >> 5) && m < P.M) {  // rows of antennas an earlier step already covered stay zero
+          steering_coeff(dv[j], ch, make_phase(P.ctot, P.ts), dt, &re, &im);
+          if (P.gain) apply_gain(gv[j], &re, &im);
+        }
+        const int Wc = static_cast<int>(__builtin_rintf(re * 16384.0f));
+        const int Ws = static_cast<int>(__builtin_rintf(im * 16384.0f));
+        const int cl = 2 * ml;
+        // (k, k + 1) = (2 sa, 2 sa + 1) are adjacent bytes of one column: one 16-bit write per (column, limb)
+        const int col_w[2][2] = {{Wc, -Ws}, {Ws, Wc}};  // [column cl + e][k = 2 sa + f]
+#pragma unroll
+        for (int ec = 0; ec < 2; ++ec) {
+          int h2[2], l2[2];
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            const int W = col_w[ec][f];
+            l2[f] = ((W + 128) & 255) - 128;
+            h2[f] = (W - l2[f]) >> 8;
+          }
+          const int off = coef8_byte(2 * sa, cl + ec, 2, 0);
+          *reinterpret_cast<uint16_t*>(lb + off) =
+              static_cast<uint16_t>((h2[0] & 255) | ((h2[1] & 255) << 8));
+          *reinterpret_cast<uint16_t*>(lb + off + 64 * 16) =
+              static_cast<uint16_t>((l2[0] & 255) | ((l2[1] & 255) << 8));
+        }
+        cs0 += Wc - Ws;  // column 2m:   W[2a][2m] + W[2a+1][2m]
+        cs1 += Ws + Wc;  // column 2m+1: W[2a][2m+1] + W[2a+1][2m+1]
+      }
+    }
+    if constexpr (!Signed) {
+      cs0 += __shfl_xor(cs0, 1);
+      cs1 += __shfl_xor(cs1, 1);
+      cs0 += __shfl_xor(cs0, 2);
+      cs1 += __shfl_xor(cs1, 2);
+      if ((lane & 3) == 0) {
+        partial[wave * 32 + 2 * (lane >> 2)] = cs0;
+        partial[wave * 32 + 2 * (lane >> 2) + 1] = cs1;
+      }
+    }
+  }
+  __syncthreads();
+
+  // unsigned samples: 128 * column sum for the lane's output columns 16 t + 4 h + r (sum of the 4 wave partials)
+  int corr[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      corr[t][r] = 0;
+      if constexpr (!Signed) {
+        const int cl = 16 * t + 4 * h + r;
+        corr[t][r] = 128 * (partial[cl] + partial[32 + cl] + partial[64 + cl] + partial[96 + cl]);
+      }
+    }
+  const float s32 = P.out_scale * 0x1p-14f;
+  const int M2 = 2 * P.M;
+  const bool full = m0 + kW8Beams <= P.M && (M2 & 15) == 0;  // 16-byte row pieces (uniform)
+
+  for (int pass = 0; pass < npasses; ++pass) {
+    const int tq = chunk * 16 + tl;
+    i32x4_t hi[2][4][2], lo[2][4][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) hi[p][i][t] = lo[p][i][t] = i32x4_t{0, 0, 0, 0};
+    for (int s = 0; s < Sp; s += 2) {  // ping-pong, unconditional clamped prefetch (exact vmcnt, see bf_wide.hip)
+      w8_contract<Signed, Mode>(lds4, s, lane, d0, hi, lo);
+      w8_load<Mode>(base, ant_stride, loff, min(s + 2, Sp - 1), P.A, d0);
+      w8_contract<Signed, Mode>(lds4, s + 1, lane, d1, hi, lo);
+      w8_load<Mode>(base, ant_stride, loff, min(s + 3, Sp - 1), P.A, d1);
+    }
+    const int next = chunk + 4;
+    if (pass + 1 < npasses) {  // next chunk's first two steps in flight during the stores
+      loff = hoff + static_cast<uint32_t>(min(next * 16 + tl, T4 - 1)) * 16u;
+      w8_load<Mode>(base, ant_stride, loff, 0, P.A, d0);
+      w8_load<Mode>(base, ant_stride, loff, 1, P.A, d1);
+    }
+    if constexpr (Mode & 4) {
+      int sum = 0;
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) sum += hi[p][i][t][0] ^ lo[p][i][t][3];
+      if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[tid] = sum;
+    } else {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint32_t pk[2][4];  // [tile][sample i] -> 4 packed int8 columns 16 t + 4 h + r
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            uint32_t packed = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              int y = (hi[p][i][t][r] << 8) + lo[p][i][t][r];
+              if constexpr (!Signed) y += corr[t][r];
+              float v = __builtin_rintf(static_cast<float>(y) * s32);
+              v = fminf(fmaxf(v, -127.0f), 127.0f);
+              packed |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(v)))) << (8 * r);
+            }
+            pk[t][i] = packed;
+          }
+        const size_t prow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T);
+        if (full) {
+          // 4x4 transpose over (h, i): lane (tl, h) gets output row 4 tq + h, columns 16 t .. 16 t + 15 -> the slab's
+          // 32 bytes of the row as two 16-byte stores
+#pragma unroll
+          for (int t = 0; t < 2; ++t) transpose_rows4(pk[t]);
+          if (tq < T4) {
+            int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 4 * tq + h) * M2 + 2 * m0;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+              *reinterpret_cast<u32x4_t*>(o + 16 * t) = u32x4_t{pk[t][0], pk[t][1], pk[t][2], pk[t][3]};
+          }
+        } else if (tq < T4) {  // partial slab / unaligned rows: byte stores with the beam guard
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 4 * tq + i) * M2 + 2 * m0;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int col = 16 * t + 4 * h + r;
+                if (2 * m0 + col < M2) o[col] = static_cast<int8_t>((pk[t][i] >> (8 * r)) & 255);
+              }
+          }
+        }
+      }
+    }
+    chunk = next;
+  }
+}
+
+template <bool Signed, int Mode = 0>
+int launch_w8(FusedArgs P, hipStream_t st) {
+  const int Sp = w8_padded_steps(P.A);
+  const size_t lds = static_cast<size_t>(Sp) * 2 * 2 * 64 * 16 + 4 * 32 * 4;
+  BF_REQUIRE(lds <= kMaxLds, "bf_beamform_fused: n_ants=%d too large for the integer wide kernel", P.A);
+  P.nslabs = (P.M + kW8Beams - 1) / kW8Beams;
+  const char* xo = getenv("BF_FUSED_XCD_ORDER");
+  P.xcd_order = P.nslabs > 1 && !(xo && xo[0] == '0');
+  const long long items = static_cast<long long>(P.B) * P.C;
+  const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
+  BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
+  hipLaunchKernelGGL((beamform_fused_i8_wide_kernel<Signed, Mode>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kW8Threads), lds, st, P);
+  BF_LAUNCHED("beamform_fused_i8_wide_kernel");
+}
+
+}  // namespace
+
+bool i8_wide_fits(const FusedArgs& P) {
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  const size_t lds = static_cast<size_t>(w8_padded_steps(P.A)) * 2 * 2 * 64 * 16 + 4 * 32 * 4;
+  return P.A >= 32 && 24 * ant_stride + static_cast<size_t>(P.T) * 4 < (1ull << 32) && lds <= kMaxLds;
+}
+
+template <bool Signed>
+int launch_i8_wide(FusedArgs P, hipStream_t st) {
+  return launch_w8<Signed>(P, st);
+}
+
+template int launch_i8_wide<false>(FusedArgs, hipStream_t);
+template int launch_i8_wide<true>(FusedArgs, hipStream_t);
+
+}  // namespace bf
+
+#ifdef BF_DIAG
+// Diagnostics: the integer wide kernel's ablations (tools/diag_fused.py, DIAG_KERNELS=w8).
+extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y, int B, int C, int T, int A, int M,
+                          int Ctot, double ts, void* stream) {
+  bf::FusedArgs P{};
+  P.raw = raw;
+  P.dv = reinterpret_cast<const float4*>(dv);
+  P.y = y;
+  P.delay_channels = 1;
+  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
+  P.ctot = Ctot;
+  P.ts = ts;
+  P.k = -3.141592653589793 / (Ctot * ts);
+  P.batch_dt = 1e-3;
+  P.out_scale = 1.0f / 64;
+  hipStream_t st = bf::as_stream(stream);
+  switch (mode) {
+    case 0: return bf::launch_w8<true, 0>(P, st);
+    case 1: return bf::launch_w8<true, 1>(P, st);
+    case 2: return bf::launch_w8<true, 2>(P, st);
+    case 4: return bf::launch_w8<true, 4>(P, st);
+    case 8: return bf::launch_w8<true, 8>(P, st);
+    case 5: return bf::launch_w8<true, 5>(P, st);
+    default: return BF_ERR_ARG;
+  }
+}
+#endif

@@ -295,7 +295,7 @@ def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C
     (4, 1, 16, 1024, 1, 16, True), (80, 24, 3, 16, 3, 1, True), (32, 8, 4, 64, 2, 1, False),
     (48, 12, 2, 128, 2, 1, False), (33, 5, 3, 80, 2, 3, True), (16, 8, 3, 48, 2, 1, True),
     (64, 16, 2, 112, 1, 1, False), (40, 32, 2, 64, 1, 2, True)])
-@pytest.mark.parametrize("i8_kernel", ["item", "generic"])
+@pytest.mark.parametrize("i8_kernel", ["item", "generic", "wide"])
 def test_fused_int8_bit_exact(context, command_queue, monkeypatch, i8_kernel, A, M, C, T, B, dch, signed):
     """int8 (requantised) beams: the integer MFMA path reproduces the oracle's integer contract bit for bit, on the
     item kernel (A <= 64, T <= 256; others fall through to generic) and the generic kernel (any A, T)."""
@@ -382,7 +382,7 @@ def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, 
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
     (64, 16, 3, 256, 2, 1, True), (64, 16, 2, 256, 2, 1, False), (19, 3, 4, 48, 2, 4, False),
     (130, 9, 2, 64, 1, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["item", "generic"])
+@pytest.mark.parametrize("i8_kernel", ["item", "generic", "wide"])
 def test_fused_int8_beam_weights_bit_exact(context, command_queue, monkeypatch, i8_kernel, A, M, C, T, B, dch, signed):
     """Weighted int8 beams: Q14 limbs of the weighted float32 coefficients, bit-exact to the integer contract."""
     monkeypatch.setenv("BF_FUSED_KERNEL", i8_kernel)

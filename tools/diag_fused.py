@@ -61,6 +61,20 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
             ts = sorted(res[mode])
             print(f"  wide tw={tw} mode {mode:2d} {wnames[mode]:18s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
                   f"alg {alg / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
+if "w8" in _os.environ.get("DIAG_KERNELS", ""):
+    lib.bf_diag_w8.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
+    w8names = {0: "full (exact coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 5: "no-coef,no-store"}
+    Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
+    alg8 = nin + nout // 4 // 4  # int8 beams: 2 B per complex beam sample vs 8
+    res = {m: [] for m in w8names}
+    for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
+        for mode in w8names:
+            res[mode].append(timeit(lambda i: lib.bf_diag_w8(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
+                                                             B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
+    for mode in w8names:
+        ts = sorted(res[mode])
+        print(f"  w8 mode {mode:2d} {w8names[mode]:18s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
+              f"alg {alg8 / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
 names_i8 = {0: "full (exact coef)", 16: "fast coef", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store",
             5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
             65: "occ 2, no-store"}
