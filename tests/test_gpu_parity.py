@@ -402,3 +402,44 @@ def test_fused_int8_beam_weights_bit_exact(context, command_queue, monkeypatch, 
     ref = O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, scale=1 / 64, signed=signed, gains=g)
     np.testing.assert_array_equal(q, ref)
     assert np.abs(ref.astype(int)).max() >= 4
+
+
+@pytest.mark.parametrize("A,M,C,T,B", [(1, 1, 1, 16, 1), (2, 1, 3, 16, 2), (16, 24, 2, 16, 1), (32, 33, 1, 32, 1),
+                                       (257, 3, 1, 16, 1)])
+@pytest.mark.parametrize("kernel", ["item", "generic", "wide"])
+def test_fused_edge_shapes(context, command_queue, monkeypatch, kernel, A, M, C, T, B):
+    """Smallest and ragged shapes on every fused path (paths that do not fit a shape fall through to one that does):
+    one antenna / beam / channel / batch, T = 16, M not a multiple of 8, A just past a k-step -- f32 within the
+    tolerance and int8 bit-exact."""
+    monkeypatch.setenv("BF_FUSED_KERNEL", kernel)
+    Ctot = 8 * C
+    d = random_delays(1, M, A, A + M)
+    rng = np.random.default_rng(A * M + T)
+    raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8)
+    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=1, delay_channels=1,
+                                 batch_dt=1e-4).instantiate(command_queue)
+    (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    assert_beams_allclose(y, O.fused_beamform(raw, d, Ctot, xeng_id=1, batch_dt=1e-4), O.reorder(raw),
+                          O.fused_tables(d, B, C, Ctot, A, xeng_id=1, batch_dt=1e-4))
+    q8 = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=1, delay_channels=1, batch_dt=1e-4,
+                                 out_int8=True, out_scale=1 / 8).instantiate(command_queue)
+    (q,) = run(q8, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    np.testing.assert_array_equal(q, O.fused_beamform_int8(raw, d, Ctot, xeng_id=1, batch_dt=1e-4, scale=1 / 8))
+
+
+@pytest.mark.parametrize("A,M,C,T,B", [(1, 1, 1, 16, 1), (3, 2, 2, 16, 1), (257, 5, 1, 32, 1)])
+def test_drop_in_edge_shapes(context, command_queue, A, M, C, T, B):
+    """The reference-structure chain (reorder -> coefficients -> table multiply) on the smallest and ragged shapes."""
+    Ctot = 4 * C
+    d = random_delays(C, M, A, 3 * A + M, rates=False)
+    raw = O.u8_voltages((B, A, C, T, 2, 2), seed=A + T)
+    seq = OpSequenceTemplate(context, B, 2, C, Ctot, T // 16, 16, A, M, 0, TS, T).instantiate(command_queue)
+    seq.ensure_all_bound()
+    seq.beamform_coeff.buffer("delay_vals").set(command_queue, d)
+    seq.prebeamform_reorder.buffer("inSamples").set(command_queue, raw)
+    seq()
+    np.testing.assert_array_equal(seq.prebeamform_reorder.buffer("outReordered").get(command_queue), O.reorder(raw))
+    np.testing.assert_array_equal(seq.beamform_coeff.buffer("outCoeffs").get(command_queue),
+                                  O.coeffs(d, B, 2, C, Ctot, A, M, 0))
+    y = seq.beamform_mult.buffer("outData").get(command_queue)
+    assert_beams_allclose(y, O.op_sequence(raw, d, C, Ctot, A, M), O.reorder(raw), O.coeffs(d, B, 2, C, Ctot, A, M, 0))
