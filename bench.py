@@ -7,7 +7,8 @@ A "step" is one pass of the hot path over one batch block of synthetic input alr
 `bf_beamform_fused` launch = pre-beamform reorder (fused) + per-batch steering-coefficient regeneration from the
 delay model + the antenna x beam complex contraction, for every (batch, pol, channel, sample) of the shard.
 Workload cfg3 (default, BASELINE configs[2], the north-star target): 64 antennas, 16 beams, 4096 channels per
-GPU, T = 256 samples, B = 8 batches, dual-pol int8 voltages, float32 beams.  cfg2 (configs[1]): 1 beam.
+GPU, T = 256 samples, B = 8 batches, dual-pol int8 voltages, int8 requantised beams from the integer MFMA path
+(bit-exact to the oracle's integer contract; `--output f32` gives float32 beams).  cfg2 (configs[1]): 1 beam.
 Frequency channels shard across ranks with no data-path collective (rank r = X-engine r, channels
 [4096 r, 4096 (r+1)) of a 4096*N-channel band): scaling is weak.
 
@@ -51,14 +52,25 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
-    p.add_argument("--out-int8", action="store_true", help="int8 requantised beams instead of float32")
+    p.add_argument("--output", choices=("int8", "f32"), default="int8",
+                   help="int8 requantised beams (bit-exact integer path, default) or float32 beams")
+    p.add_argument("--out-int8", action="store_true", help="same as --output int8")
+    p.add_argument("--out-f32", action="store_true", help="same as --output f32")
+    p.add_argument("--settle-ms", type=float, default=300.0,
+                   help="untimed clock-settle launches after the warmup steps (milliseconds of wall time)")
     p.add_argument("--unsigned", action="store_true", help="uint8 voltages (the reference slots' dtype) instead of int8")
     p.add_argument("--nbuf", type=int, default=2, help="rotating input/output buffer sets (defeat the 256 MB MALL)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-secondary", action="store_true")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    return p.parse_args()
+    a = p.parse_args()
+    if a.out_f32:
+        a.output = "f32"
+    if a.out_int8:
+        a.output = "int8"
+    a.out_int8 = a.output == "int8"
+    return a
 
 
 class Dist:
@@ -139,6 +151,16 @@ def run_gpu(args, dist, wl):
     for i in range(args.warmup):
         ops[i % len(ops)]()
     queue.finish()
+    # Clock settle (untimed, before the timed region): the GPU ramps its clocks over the first ~30 ms of load
+    # (the first launches of a fresh process run up to 35 % slower, profiles/r1_v6_clock_ramp.txt); a streaming
+    # beamformer runs continuously, so the steady state is the number that matters.
+    t_settle = time.perf_counter()
+    i = 0
+    while time.perf_counter() - t_settle < args.settle_ms / 1e3:
+        for _ in range(8):
+            ops[i % len(ops)]()
+            i += 1
+        queue.finish()
 
     e0, e1 = accel.Event(), accel.Event()
     dist.barrier()
@@ -160,7 +182,7 @@ def run_gpu(args, dist, wl):
                 out=(ops, queue))
 
 
-def cpu_baseline(wl, seconds=10.0):
+def cpu_baseline(wl, out_int8, seconds=10.0):
     """The oracle's vectorised NumPy restatement (reorder -> per-batch coefficients -> f32 matmul) timed on
     this host on a bounded channel sample of the same workload (kind "port")."""
     import numpy as np
@@ -181,7 +203,9 @@ def cpu_baseline(wl, seconds=10.0):
         raw = rng.integers(-128, 128, size=(B, A, c, T, 2, 2), dtype=np.int8)
         t = time.perf_counter()
         Ctot = wl.get("Ctot", wl["C"])
-        O.fused_beamform(raw, d, Ctot, signed=True, batch_dt=T * 2 * Ctot * TS)
+        y = O.fused_beamform(raw, d, Ctot, signed=True, batch_dt=T * 2 * Ctot * TS)
+        if out_int8:
+            O.requantise(y, 1 / 64)
         return time.perf_counter() - t
 
     c = 16
@@ -191,7 +215,8 @@ def cpu_baseline(wl, seconds=10.0):
     rate = A * 2 * c * T * B / dt / 1e9
     return {"value": round(rate, 4), "unit": "Gsamples/s", "cores": int(threads), "kind": "port",
             "sample": f"{c} of {wl['C']} channels x B={B} x T={T} x A={A} x 2 pols ({dt:.1f} s): oracle.fused_beamform "
-                      f"(NumPy reorder + float64-phase coefficients + float32 matmul, BLAS threads={threads})"}
+                      f"(NumPy reorder + float64-phase coefficients + float32 matmul{' + requantise' if out_int8 else ''}, "
+                      f"BLAS threads={threads})"}
 
 
 def pmc_traffic(args):
@@ -205,7 +230,7 @@ def pmc_traffic(args):
         out = tempfile.mkdtemp(prefix="bfpmc_", dir=os.environ.get("TMPDIR", "/tmp"))
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
-               "--steps", "3", "--warmup", "1"] + (["--out-int8"] if args.out_int8 else []) + \
+               "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--output", args.output] + \
               (["--unsigned"] if args.unsigned else [])
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
@@ -227,6 +252,25 @@ KERNELS = {False: ("beamform_fused_item_kernel",
                   "f16 hi/lo-split coefficients on v_mfma_f32_16x16x32_f16, f32 accumulation"),
            True: ("beamform_fused_i8_item_kernel",
                   "Q14 two-limb int8 coefficients on v_mfma_i32_16x16x64_i8, exact int32 accumulation, int8 beams")}
+
+
+MFMA_PEAK = {True: (5000.0, "TOPS", "v_mfma_i32_16x16x64_i8 (2x the dense BF16 rate, MI355X_MICROARCH.md)"),
+             False: (2500.0, "TFLOP/s", "v_mfma_f32_16x16x32_f16 (dense F16 = BF16 rate)")}
+
+
+def mfma_util(wl, out_int8, kernel_s):
+    """Matrix-core utilisation of the dominant kernel: algorithmic ops (8 A M per (b, p, c, t): the complex MAC)
+    and the ops the MFMAs actually issue (two coefficient limbs, K = 2A padded to the MFMA depth, N = 2M padded
+    to 16), both against the dense peak.  The path is HBM-bound by design (SURVEY §7 hard part 1): this shows the
+    headroom, not a target."""
+    A, M, C, T, B = wl["A"], wl["M"], wl["C"], wl["T"], wl["B"]
+    kg = 64 if out_int8 else 32
+    kpad, npad = -(-2 * A // kg) * kg, -(-2 * M // 16) * 16
+    alg = 8.0 * A * M * 2 * C * T * B
+    issued = 2.0 * 2 * kpad * npad * T * 2 * C * B
+    peak, unit, instr = MFMA_PEAK[out_int8]
+    return {"instruction": instr, "unit": unit, "peak": peak, "algorithmic": round(alg / kernel_s / 1e12, 1),
+            "issued": round(issued / kernel_s / 1e12, 1), "frac_issued": round(issued / kernel_s / 1e12 / peak, 4)}
 
 
 def kernel_name(wl, out_int8):
@@ -276,6 +320,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": kernel_name(wl, args.out_int8), "avg_launch_us": round(r["kernel_s"] * 1e6, 2),
                      "alg_bytes_per_launch": r["alg_bytes"]},
+        "mfma": mfma_util(wl, args.out_int8, r["kernel_s"]),
         "cpu_baseline": None,
     }
     del ops_queue
@@ -295,7 +340,7 @@ def main():
         except Exception as e:
             line["roofline"]["traffic_counters"] = f"unavailable: {str(e)[:200]}"
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(wl)
+        line["cpu_baseline"] = cpu_baseline(wl, args.out_int8)
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     dist.close()

@@ -506,8 +506,7 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_kernel(FusedArgs P) {
 
 
 
-__device__ __forceinline__ void put_q14(int8_t* lb, int* colsum, int k, int cl, int nts, float w) {
-  const int W = static_cast<int>(__builtin_rintf(w * 16384.0f));  // exact product, RNE
+__device__ __forceinline__ void put_q14(int8_t* lb, int* colsum, int k, int cl, int nts, int W) {
   const int lo = ((W + 128) & 255) - 128;
   const int hi = (W - lo) >> 8;
   lb[coef8_byte(k, cl, nts, 0)] = static_cast<int8_t>(hi);
@@ -535,7 +534,7 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P
   int* colsum = reinterpret_cast<int*>(lb + static_cast<size_t>(S8) * nts * 2 * 64 * 16);
   const int M2 = 2 * P.M;
 
-  // 1. coefficients (exact float64 phasors) -> Q14 limbs + column sums
+  // 1. coefficients (Q14 of the exact phasors, bf_phase.hpp q14_coeffs) -> limbs + column sums
   for (int e = tid; e < nts * 16; e += kThreads) colsum[e] = 0;
   __syncthreads();
   {
@@ -547,17 +546,16 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P
     for (int e = tid; e < npairs; e += kThreads) {
       const int a = e / nbeam, ml = e - a * nbeam;
       const int m = tau0 * 8 + ml;
-      float re = 0.0f, im = 0.0f;
-      if (a < P.A && m < P.M) {
-        steering_coeff(P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a], ch, make_phase(P.ctot, P.ts), dt, &re,
-                       &im);
-        if (P.gain) apply_gain(P.gain[m * P.A + a], &re, &im);
-      }
+      const bool valid[1] = {a < P.A && m < P.M};
+      const float4 dv[1] = {P.dv[(static_cast<size_t>(cd) * P.M + min(m, P.M - 1)) * P.A + min(a, P.A - 1)]};
+      const float g[1] = {P.gain ? P.gain[min(m, P.M - 1) * P.A + min(a, P.A - 1)] : 1.0f};
+      int wc[1], ws[1];
+      q14_coeffs<1>(dv, g, valid, ch, P.ctot, P.ts, P.k, dt, P.gain, wc, ws);
       const int cl = 2 * ml;
-      put_q14(lb, colsum, 2 * a, cl, nts, re);
-      put_q14(lb, colsum, 2 * a, cl + 1, nts, im);
-      put_q14(lb, colsum, 2 * a + 1, cl, nts, -im);
-      put_q14(lb, colsum, 2 * a + 1, cl + 1, nts, re);
+      put_q14(lb, colsum, 2 * a, cl, nts, wc[0]);
+      put_q14(lb, colsum, 2 * a, cl + 1, nts, ws[0]);
+      put_q14(lb, colsum, 2 * a + 1, cl, nts, -ws[0]);
+      put_q14(lb, colsum, 2 * a + 1, cl + 1, nts, wc[0]);
     }
   }
   __syncthreads();
@@ -681,7 +679,7 @@ __device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* cols
 // voltages (16 x 16 B per lane) -> exact coefficients + Q14 limbs under them -> barrier -> per pol: v_perm
 // fragments, 8 i8 MFMAs per (sample, tile), requantise, 4-byte stores.
 // Mode (diagnostics only): kSkipCoef / kSkipMfma / kSkipStore / kSkipLoad as the float item kernel; 16 = fast
-// (f32 sincos) coefficients instead of exact.
+// (f32 sincos) coefficients only (inexact); 128 = exact coefficients only (no fast attempt).
 template <bool Signed, int NTS, bool Full, int Mode = 0>
 __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
@@ -738,36 +736,53 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
     const double ch = static_cast<double>(P.base_ch + c);
     // this thread's contributions to columns 2ml, 2ml+1: ml = tid % nbeam for every pair it owns (256 % nbeam == 0)
     int cs0 = 0, cs1 = 0;
+    constexpr int NP = CoefPrefetch<NTS>::kMaxPairs;
+    bool valid[NP];
+    int wc[NP], ws[NP];
 #pragma unroll
-    for (int j = 0; j < CoefPrefetch<NTS>::kMaxPairs; ++j) {
+    for (int j = 0; j < NP; ++j) {
+      const int e = tid + j * kThreads;
+      const int a = e / nbeam, m = tau0 * 8 + (e - a * nbeam);
+      valid[j] = e < npairs && a < P.A && m < P.M;
+    }
+    if constexpr (Mode & kSkipCoef) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        wc[j] = 8192 + 16 * j + tid;
+        ws[j] = 4096 - 16 * j;
+      }
+    } else if constexpr (Mode & 16) {  // diagnostics: float32 phasors only (not the contract)
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        float re, im;
+        steering_coeff_fast(cp.dv[j], ch - P.ctot / 2.0, P.k, dt, &re, &im);
+        wc[j] = static_cast<int>(__builtin_rintf(re * 16384.0f));
+        ws[j] = static_cast<int>(__builtin_rintf(im * 16384.0f));
+      }
+    } else {
+      q14_coeffs<NP, !(Mode & 128)>(cp.dv, cp.g, valid, ch, P.ctot, P.ts, P.k, dt, P.gain, wc, ws);
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
       const int e = tid + j * kThreads;
       if (e >= npairs) break;
       const int a = e / nbeam, ml = e - a * nbeam;
-      const int m = tau0 * 8 + ml;
-      float re = 0.0f, im = 0.0f;
-      if constexpr (Mode & kSkipCoef) {
-        re = 0.5f + 1e-3f * a;
-        im = 0.25f - 1e-3f * m;
-      } else if (a < P.A && m < P.M) {
-        if constexpr (Mode & 16) {
-          steering_coeff_fast(cp.dv[j], ch - P.ctot / 2.0, P.k, dt, &re, &im);
-        } else {
-          steering_coeff(cp.dv[j], ch, make_phase(P.ctot, P.ts), dt, &re, &im);
-        }
-        if (P.gain) apply_gain(cp.g[j], &re, &im);
-      }
+      const int Wc = wc[j], Ws = ws[j];
       const int cl = 2 * ml;
-      const int Wc = static_cast<int>(__builtin_rintf(re * 16384.0f));
-      const int Ws = static_cast<int>(__builtin_rintf(im * 16384.0f));
-      const int ks[4] = {2 * a, 2 * a, 2 * a + 1, 2 * a + 1};
-      const int cs[4] = {cl, cl + 1, cl, cl + 1};
-      const int ws[4] = {Wc, Ws, -Ws, Wc};
+      // (k, k + 1) = (2a, 2a + 1) are adjacent bytes of one column: one 16-bit write per (column, limb)
+      const int col_w[2][2] = {{Wc, -Ws}, {Ws, Wc}};  // [column cl + ec][k = 2a + f]
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int lo = ((ws[r] + 128) & 255) - 128;
-        const int hi = (ws[r] - lo) >> 8;
-        lb[coef8_byte(ks[r], cs[r], nts, 0)] = static_cast<int8_t>(hi);
-        lb[coef8_byte(ks[r], cs[r], nts, 1)] = static_cast<int8_t>(lo);
+      for (int ec = 0; ec < 2; ++ec) {
+        int h2[2], l2[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          l2[f] = ((col_w[ec][f] + 128) & 255) - 128;
+          h2[f] = (col_w[ec][f] - l2[f]) >> 8;
+        }
+        *reinterpret_cast<uint16_t*>(lb + coef8_byte(2 * a, cl + ec, nts, 0)) =
+            static_cast<uint16_t>((h2[0] & 255) | ((h2[1] & 255) << 8));
+        *reinterpret_cast<uint16_t*>(lb + coef8_byte(2 * a, cl + ec, nts, 1)) =
+            static_cast<uint16_t>((l2[0] & 255) | ((l2[1] & 255) << 8));
       }
       cs0 += Wc - Ws;  // column 2m:   W[2a][2m] + W[2a+1][2m]
       cs1 += Ws + Wc;  // column 2m+1: W[2a][2m+1] + W[2a+1][2m+1]
@@ -1229,6 +1244,7 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 7: return bf::launch_i8_item<true, 2, true, 7>(P, st);
       case 8: return bf::launch_i8_item<true, 2, true, 8>(P, st);
       case 16: return bf::launch_i8_item<true, 2, true, 16>(P, st);
+      case 128: return bf::launch_i8_item<true, 2, true, 128>(P, st);
       case 32: return bf::launch_i8_item<true, 2, true, 32>(P, st);
       case 64: return bf::launch_i8_item<true, 2, true, 0>(P, st, 60 * 1024);  // occupancy 2 (LDS-limited)
       case 65: return bf::launch_i8_item<true, 2, true, 4>(P, st, 60 * 1024);

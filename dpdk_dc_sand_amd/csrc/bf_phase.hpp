@@ -89,7 +89,9 @@ __device__ __forceinline__ void steering_coeff(float4 dv, double ch, const Phase
 // first-order correction for rf's float32 rounding dr = r - rf, and the quadrant swap.  <= 1.32 ulp of float32 (mean
 // |error| 2e-8) against the exact phasor over 2e7 probe angles (tools/probes/sincosf_check.c), about a third of the
 // instructions of the generic sincosf (which redoes a general range reduction).
-__device__ __forceinline__ void steering_coeff_fast(float4 dv, double chc, double k, double dt, float* re, float* im) {
+// Returns the float64 rotation (callers that need a validity range check it).
+__device__ __forceinline__ double steering_coeff_fast(float4 dv, double chc, double k, double dt, float* re,
+                                                      float* im) {
   double tau = static_cast<double>(dv.x);
   double phi = static_cast<double>(dv.z);
   if (dt != 0.0) {
@@ -111,6 +113,122 @@ __device__ __forceinline__ void steering_coeff_fast(float4 dv, double chc, doubl
   const float s0 = (q & 1) ? c1 : s1, c0 = (q & 1) ? s1 : c1;
   *re = ((q + 1) & 2) ? -c0 : c0;
   *im = (q & 2) ? -s0 : s0;
+  return rot;
+}
+
+// ---- Q14 phasors of the integer (int8-beam) path ----------------------------------------------------------------
+// Contract (oracle fused_beamform_int8): W = (rint(2^14 re), rint(2^14 im)) of the EXACT phasor (steering_coeff,
+// then the optional gain), ties to even.  q14_fast evaluates the phasor to ~1e-10 instead: float64 rotation without
+// divisions, Cody-Waite reduction, cos/sin with the leading Taylor terms in float64 and the tails (< 4e-4) in
+// float32, so |v - cos(rot_exact)| <= 2.4e-10 (tools/probes/q14_fast_check.c: 2e7 arguments, delays up to 2e5
+// samples) < kQ14Eps.  The exact float32 phasor component is then RN32(v -+ eps) -- one of two adjacent floats --
+// and when both give the same Q14 value (after the gain, as the contract applies it) that value IS the contract's.
+// Otherwise (1.6e-5 of the components), or for a NaN / out-of-range argument, q14_fast returns false and the caller
+// re-evaluates that coefficient exactly: bit-exact at little more than the cost of the float32 phasor.
+constexpr double kQ14Eps = 5e-10;
+constexpr float kQ14MaxMag = 2e5f;  // |tau'| (ch + Ctot/2) |K| + |phi'| bound of the error analysis above
+
+__device__ __forceinline__ int q14_pair(double v, float g, bool gained, bool* ok) {
+  float a = static_cast<float>(v - kQ14Eps), b = static_cast<float>(v + kQ14Eps);
+  if (gained) {
+    a = __fmul_rn(a, g);
+    b = __fmul_rn(b, g);
+  }
+  const int qa = static_cast<int>(__builtin_rintf(a * 16384.0f)), qb = static_cast<int>(__builtin_rintf(b * 16384.0f));
+  *ok = *ok && qa == qb;
+  return qa;
+}
+
+// uk = (ch + Ctot/2) * |K| (uniform per item), for the range check.
+__device__ __forceinline__ bool q14_fast(float4 dv, double chc, double k, double dt, float uk, float g, bool gained,
+                                         int* wc, int* ws) {
+  double tau = static_cast<double>(dv.x);
+  double phi = static_cast<double>(dv.z);
+  if (dt != 0.0) {
+    tau = fma(static_cast<double>(dv.y), dt, tau);
+    phi = fma(static_cast<double>(dv.w), dt, phi);
+  }
+  const double rot = fma(tau * chc, k, phi);
+  const double n = rint(rot * 0.63661977236758138);  // 2 / pi
+  double r = fma(-n, 1.5707963267948966e+00, rot);
+  r = fma(-n, 6.123233995736766e-17, r);
+  const double z = r * r;
+  const float zf = static_cast<float>(z);
+  // cos r = 1 - z/2 + z^2/24 - z^3 (1/720 - z/40320 + z^2/3628800 - z^3/479001600)
+  const float tc = zf * zf * zf *
+                   fmaf(fmaf(fmaf(2.0876757e-09f, zf, -2.7557319e-07f), zf, 2.4801587e-05f), zf, -1.3888889e-03f);
+  const double cz = fma(z * z, 4.1666666666666664e-02, fma(z, -0.5, 1.0)) + static_cast<double>(tc);
+  // sin r = r - r z/6 + r z^2/120 - r z^3 (1/5040 - z/362880 + z^2/39916800 - z^3/6227020800)
+  const double rz = r * z, rz2 = rz * z;
+  const float tsn = static_cast<float>(rz2) * zf *
+                    fmaf(fmaf(fmaf(-1.6059044e-10f, zf, 2.5052108e-08f), zf, -2.7557319e-06f), zf, 1.9841270e-04f);
+  const double sz = fma(rz2, 8.3333333333333332e-03, fma(rz, -1.6666666666666666e-01, r)) - static_cast<double>(tsn);
+  const int q = static_cast<int>(static_cast<long long>(n) & 3);
+  const double s0 = (q & 1) ? cz : sz, c0 = (q & 1) ? sz : cz;
+  const double cv = ((q + 1) & 2) ? -c0 : c0;
+  const double sv = (q & 2) ? -s0 : s0;
+  const float mag = fabsf(static_cast<float>(tau)) * uk + fabsf(static_cast<float>(phi));
+  bool ok = mag < kQ14MaxMag;  // false for NaN too
+  *wc = q14_pair(cv, g, gained, &ok);
+  *ws = q14_pair(sv, g, gained, &ok);
+  return ok;
+}
+
+// The exact evaluation (the contract itself): float64 phase in the reference's order, float32 rounding, gain.
+__device__ __forceinline__ void q14_exact(float4 dv, double ch, double ctot, double ts, double dt, const float* gain,
+                                          float g, int* wc, int* ws) {
+  float re, im;
+  steering_coeff(dv, ch, make_phase(ctot, ts), dt, &re, &im);
+  if (gain) {
+    re = __fmul_rn(re, g);
+    im = __fmul_rn(im, g);
+  }
+  *wc = static_cast<int>(__builtin_rintf(re * 16384.0f));
+  *ws = static_cast<int>(__builtin_rintf(im * 16384.0f));
+}
+
+// N coefficients per lane: fast for all, then an exact pass per flagged coefficient (a wave runs as many exact
+// passes as its most-flagged lane has flags: usually none).  valid[j] false -> W = 0.  FastFirst = false is the
+// exact-only form (diagnostics / ablation).
+template <int N, bool FastFirst = true>
+__device__ __forceinline__ void q14_coeffs(const float4 (&dv)[N], const float (&g)[N], const bool (&valid)[N],
+                                           double ch, double ctot, double ts, double k, double dt, const float* gain,
+                                           int (&wc)[N], int (&ws)[N]) {
+  const double chc = ch - ctot / 2.0;
+  const float uk = static_cast<float>((ch + ctot / 2.0) * fabs(k));
+  unsigned flagged = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    wc[j] = ws[j] = 0;
+    if (!valid[j]) continue;
+    if constexpr (FastFirst) {
+      if (!q14_fast(dv[j], chc, k, dt, uk, g[j], gain != nullptr, &wc[j], &ws[j])) flagged |= 1u << j;
+    } else {
+      flagged |= 1u << j;
+    }
+  }
+  while (flagged) {
+    const int j = __builtin_ctz(flagged);
+    flagged &= flagged - 1;
+    float4 d = dv[0];
+    float gj = g[0];
+#pragma unroll
+    for (int jj = 1; jj < N; ++jj) {  // register selects (no dynamic indexing: that would go to scratch)
+      const bool hit = j == jj;
+      d.x = hit ? dv[jj].x : d.x;
+      d.y = hit ? dv[jj].y : d.y;
+      d.z = hit ? dv[jj].z : d.z;
+      d.w = hit ? dv[jj].w : d.w;
+      gj = hit ? g[jj] : gj;
+    }
+    int c, s;
+    q14_exact(d, ch, ctot, ts, dt, gain, gj, &c, &s);
+#pragma unroll
+    for (int jj = 0; jj < N; ++jj) {
+      wc[jj] = j == jj ? c : wc[jj];
+      ws[jj] = j == jj ? s : ws[jj];
+    }
+  }
 }
 
 }  // namespace bf

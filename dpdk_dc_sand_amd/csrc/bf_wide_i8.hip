@@ -144,24 +144,32 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(F
         gv[j] = 1.0f;
         if (P.gain) gv[j] = P.gain[m * P.A + a];
       }
+      bool valid[kBatch];
+      int wc[kBatch], ws[kBatch];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int e = e0 + j * kW8Threads;
+        const int sa = 4 * ((e >> 2) / kW8Beams) + (e & 3);
+        const int a = w8_step_base(sa >> 5, P.A) + (sa & 31);
+        // rows of antennas an earlier step already covered stay zero
+        valid[j] = e < npairs && a >= 32 * (sa >> 5) && m0 + (e >> 2) % kW8Beams < P.M;
+      }
+      if constexpr (Mode & 1) {
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+          wc[j] = 8192 + 16 * j + tid;
+          ws[j] = 4096 - 16 * j;
+        }
+      } else {
+        q14_coeffs<kBatch, !(Mode & 128)>(dv, gv, valid, ch, P.ctot, P.ts, P.k, dt, P.gain, wc, ws);
+      }
 #pragma unroll
       for (int j = 0; j < kBatch; ++j) {
         const int e = e0 + j * kW8Threads;
         if (e >= npairs) break;
         const int ml = (e >> 2) % kW8Beams;
         const int sa = 4 * ((e >> 2) / kW8Beams) + (e & 3);
-        const int a = w8_step_base(sa >> 5, P.A) + (sa & 31);
-        const int m = m0 + ml;
-        float re = 0.0f, im = 0.0f;
-        if constexpr (Mode & 1) {
-          re = 0.5f + 1e-3f * a;
-          im = 0.25f - 1e-3f * m;
-        } else if (a >= 32 * (sa >> 5) && m < P.M) {  // rows of antennas an earlier step already covered stay zero
-          steering_coeff(dv[j], ch, make_phase(P.ctot, P.ts), dt, &re, &im);
-          if (P.gain) apply_gain(gv[j], &re, &im);
-        }
-        const int Wc = static_cast<int>(__builtin_rintf(re * 16384.0f));
-        const int Ws = static_cast<int>(__builtin_rintf(im * 16384.0f));
+        const int Wc = wc[j], Ws = ws[j];
         const int cl = 2 * ml;
         // (k, k + 1) = (2 sa, 2 sa + 1) are adjacent bytes of one column: one 16-bit write per (column, limb)
         const int col_w[2][2] = {{Wc, -Ws}, {Ws, Wc}};  // [column cl + e][k = 2 sa + f]
@@ -350,6 +358,7 @@ extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y
     case 4: return bf::launch_w8<true, 4>(P, st);
     case 8: return bf::launch_w8<true, 8>(P, st);
     case 5: return bf::launch_w8<true, 5>(P, st);
+    case 128: return bf::launch_w8<true, 128>(P, st);  // exact phasors only (no fast attempt)
     default: return BF_ERR_ARG;
   }
 }

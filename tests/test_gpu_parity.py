@@ -404,6 +404,50 @@ def test_fused_int8_beam_weights_bit_exact(context, command_queue, monkeypatch, 
     assert np.abs(ref.astype(int)).max() >= 4
 
 
+def boundary_delays(M, A, seed):
+    """Zero delays (rot = phase exactly) with phases whose cos or sin lands within ~1e-7 of a Q14 rounding
+    boundary (k + 1/2) / 2^14: the fast float32 phasor cannot decide those, so nearly every coefficient takes
+    the exact fallback (several per lane), and some with a gain too."""
+    rng = np.random.default_rng(seed)
+    k = rng.integers(-16000, 16000, (M, A))
+    target = (k + 0.5) / 16384.0
+    phi = np.arccos(target)
+    use_sin = rng.random((M, A)) < 0.5
+    phi = np.where(use_sin, np.pi / 2 - phi, phi)  # sin(pi/2 - x) = cos(x)
+    phi = np.where(rng.random((M, A)) < 0.5, -phi, phi)
+    d = np.zeros((1, M, A, 4), np.float32)
+    d[0, ..., 2] = phi.astype(np.float32)
+    return d
+
+
+@pytest.mark.parametrize("A,M,C,T,B,signed", [(64, 16, 3, 256, 2, True), (64, 16, 2, 256, 2, False),
+                                              (19, 3, 3, 48, 2, False), (256, 64, 1, 32, 1, True)])
+@pytest.mark.parametrize("i8_kernel", ["item", "generic", "wide"])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_fused_int8_rounding_boundaries(context, command_queue, monkeypatch, i8_kernel, weighted, A, M, C, T, B,
+                                        signed):
+    """Q14 coefficients whose exact value sits at a rounding boundary: the fast-phasor + exact-fixup path
+    (bf_phase.hpp q14_coeffs) must still reproduce the integer contract bit for bit."""
+    monkeypatch.setenv("BF_FUSED_KERNEL", i8_kernel)
+    Ctot, xeng, t0, bdt = 4096, 0, 1e-3, 256 * 8192 * TS
+    d = boundary_delays(M, A, A + M)
+    rng = np.random.default_rng(A * 5 + M)
+    raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8)
+    if signed:
+        raw = raw.view(np.int8)
+    g = rng.choice(np.float32([1.0, 0.5, -1.0, 0.75]), (M, A)).astype(np.float32) if weighted else None
+    op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=signed,
+                                 out_int8=True, out_scale=1 / 64, t0=t0, batch_dt=bdt,
+                                 beam_weights=weighted).instantiate(command_queue)
+    if weighted:
+        for m in range(M):
+            op.set_beam_weights(m, g[m])
+    (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    ref = O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, scale=1 / 64, signed=signed,
+                                gains=g)
+    np.testing.assert_array_equal(q, ref)
+
+
 @pytest.mark.parametrize("A,M,C,T,B", [(1, 1, 1, 16, 1), (2, 1, 3, 16, 2), (16, 24, 2, 16, 1), (32, 33, 1, 32, 1),
                                        (257, 3, 1, 16, 1)])
 @pytest.mark.parametrize("kernel", ["item", "generic", "wide"])

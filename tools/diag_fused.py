@@ -26,7 +26,16 @@ for xi, yo in bufs:  # random voltages: constant data runs at a higher clock (MI
     else:
         xi.set(q, _rng.integers(0, 256, nin, dtype=np.uint8))
 dv = accel.DeviceArray(ctx, (M * A * 4,), np.float32)
-dv.set(q, np.random.default_rng(0).uniform(0, 1e-8, M * A * 4).astype(np.float32))
+_drng = np.random.default_rng(0)
+if _os.environ.get("DIAG_DV", "bench") == "tiny":  # near-zero phases: constant (1, 0) phasors, higher clocks
+    dv.set(q, _drng.uniform(0, 1e-8, M * A * 4).astype(np.float32))
+else:  # the bench's delay model (random phasors: realistic MFMA operand toggling / power)
+    _d = np.zeros((M, A, 4), np.float32)
+    _d[..., 0] = _drng.uniform(0, 10 / 1712e6, (M, A))
+    _d[..., 1] = _drng.uniform(-1e-9, 1e-9, (M, A))
+    _d[..., 2] = _drng.uniform(-np.pi, np.pi, (M, A))
+    _d[..., 3] = _drng.uniform(-1, 1, (M, A))
+    dv.set(q, _d.reshape(-1))
 alg = nin + nout
 
 
@@ -63,7 +72,7 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
                   f"alg {alg / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
 if "w8" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_w8.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
-    w8names = {0: "full (exact coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 5: "no-coef,no-store"}
+    w8names = {0: "full (fast+fixup)", 128: "exact-only coef", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 5: "no-coef,no-store"}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
     alg8 = nin + nout // 4 // 4  # int8 beams: 2 B per complex beam sample vs 8
     res = {m: [] for m in w8names}
@@ -75,7 +84,7 @@ if "w8" in _os.environ.get("DIAG_KERNELS", ""):
         ts = sorted(res[mode])
         print(f"  w8 mode {mode:2d} {w8names[mode]:18s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
               f"alg {alg8 / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
-names_i8 = {0: "full (exact coef)", 16: "fast coef", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store",
+names_i8 = {0: "full (fast+fixup coef)", 128: "exact-only coef", 16: "fast coef (inexact)", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store",
             5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
             65: "occ 2, no-store"}
 alg_i8 = nin + nout // 4
