@@ -32,6 +32,11 @@ constexpr int kSkipCoef = 1, kSkipMfma = 2, kSkipStore = 4, kSkipLoad = 8;
 // time, profiles/r1_v2_ablation_nt.txt); kCachedLoad selects plain loads, kNtStore non-temporal beam stores
 // (slower: +17 %).
 constexpr int kCachedLoad = 128, kNtStore = 256;
+// Integer item kernel layout variants (A/B-measured in the diagnostic build, profiles/r1_v7_i8_variants.txt):
+// kSerialCoef evaluates the fast Q14 phasors one at a time (fewer live float64 temporaries: no gain), kPolOrder
+// restores the pol-outermost contraction of full slabs (the product runs sample-row-outermost with immediate
+// requantisation: -1.3 % at 3 waves per SIMD).
+constexpr int kSerialCoef = 1024, kPolOrder = 2048;
 
 // One group of 4 k-steps: 16 x 16-byte loads per lane, all UNCONDITIONAL: out-of-range antennas (a >= A) read
 // antenna A-1 and meet zero coefficient rows, out-of-range time quads read the last quad and are never stored,
@@ -633,15 +638,14 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P
         for (int tau = 0; tau < NTS; ++tau) {
           if (tau >= nts) break;
           const int col0 = 16 * (tau0 + tau) + 4 * h;
-          uint32_t packed = 0;
+          uint32_t qb[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             int y = acc[p][i][tau][r];
             if constexpr (!Signed) y += 128 * colsum[16 * tau + 4 * h + r];  // x = (x - 128) + 128
-            float v = __builtin_rintf(static_cast<float>(y) * s32);
-            v = fminf(fmaxf(v, -127.0f), 127.0f);
-            packed |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(v)))) << (8 * r);
+            qb[r] = requant_bits(y, s32);
           }
+          const uint32_t packed = pack_low_bytes(qb[0], qb[1], qb[2], qb[3]);
           if ((M2 & 3) == 0 && col0 + 4 <= M2) {
             *reinterpret_cast<uint32_t*>(o + col0) = packed;
           } else {
@@ -659,7 +663,7 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P
 // q = clamp(rne(f32(y) * f32(scale * 2^-14)), +-127); unsigned input adds back 128 * column sum (4 wave partials).
 template <bool Signed>
 __device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* colsum, int cl0, float s32) {
-  uint32_t packed = 0;
+  uint32_t q[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     int y = acc[r];
@@ -667,11 +671,9 @@ __device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* cols
       const int cl = cl0 + r;
       y += 128 * (colsum[cl] + colsum[32 + cl] + colsum[64 + cl] + colsum[96 + cl]);
     }
-    float v = __builtin_rintf(static_cast<float>(y) * s32);
-    v = fminf(fmaxf(v, -127.0f), 127.0f);
-    packed |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(v)))) << (8 * r);
+    q[r] = requant_bits(y, s32);
   }
-  return packed;
+  return pack_low_bytes(q[0], q[1], q[2], q[3]);
 }
 
 
@@ -680,8 +682,8 @@ __device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* cols
 // fragments, 8 i8 MFMAs per (sample, tile), requantise, 4-byte stores.
 // Mode (diagnostics only): kSkipCoef / kSkipMfma / kSkipStore / kSkipLoad as the float item kernel; 16 = fast
 // (f32 sincos) coefficients only (inexact); 128 = exact coefficients only (no fast attempt).
-template <bool Signed, int NTS, bool Full, int Mode = 0>
-__global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedArgs P) {
+template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3>
+__global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
@@ -760,7 +762,8 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
         ws[j] = static_cast<int>(__builtin_rintf(im * 16384.0f));
       }
     } else {
-      q14_coeffs<NP, !(Mode & 128)>(cp.dv, cp.g, valid, ch, P.ctot, P.ts, P.k, dt, P.gain, wc, ws);
+      q14_coeffs<NP, !(Mode & 128), (Mode & kSerialCoef) != 0>(cp.dv, cp.g, valid, ch, P.ctot, P.ts, P.k, dt,
+                                                                 P.gain, wc, ws);
     }
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
@@ -803,12 +806,66 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
   const int4* fr = reinterpret_cast<const int4*>(lds);
   const float s32 = P.out_scale * 0x1p-14f;
 
+  // Full slabs: sample row i outermost, both pols inside, each 4-MFMA chain requantised at once, so only the
+  // packed bytes (16 VGPRs) stay live and the voltage registers of row i die after it.
+  constexpr bool kTile = Full && !(Mode & (kSkipMfma | kSkipStore | kSkipLoad | kPolOrder));
+  uint32_t pkall[2][NTS][4];
+  if constexpr (kTile) {
+    i32x4_t chi[2][NTS], clo[2][NTS];
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int tau = 0; tau < NTS; ++tau) {
+        if (ss < S8) {
+          const int4 x0 = fr[(((ss * NTS + tau) * 2 + 0) * 64) + lane];
+          const int4 x1 = fr[(((ss * NTS + tau) * 2 + 1) * 64) + lane];
+          chi[ss][tau] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
+          clo[ss][tau] = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+        } else {
+          chi[ss][tau] = clo[ss][tau] = i32x4_t{0, 0, 0, 0};
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const uint32_t sel = p ? kSelP1 : kSelP0;
+        i32x4_t f[2];
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          uint32_t w[4];
+#pragma unroll
+          for (int m2 = 0; m2 < 4; ++m2) {
+            uint32_t lo = d[ss][2 * m2][i], hi = d[ss][2 * m2 + 1][i];
+            if constexpr (!Signed) {
+              lo ^= 0x80808080u;
+              hi ^= 0x80808080u;
+            }
+            w[m2] = __builtin_amdgcn_perm(hi, lo, sel);
+          }
+          f[ss] = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]),
+                          static_cast<int>(w[3])};
+        }
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau) {
+          i32x4_t t = mfma_i8(chi[0][tau], f[0], i32x4_t{0, 0, 0, 0});
+          t = mfma_i8(chi[1][tau], f[1], t);
+          t = t << 8;
+          t = mfma_i8(clo[0][tau], f[0], t);
+          t = mfma_i8(clo[1][tau], f[1], t);
+          pkall[p][tau][i] = requant4<Signed>(t, colsum, 16 * tau + 4 * h, s32);
+        }
+      }
+    }
+  }
+
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const uint32_t sel = p ? kSelP1 : kSelP0;
     i32x4_t acc[4][NTS];
 #pragma unroll
     for (int tau = 0; tau < NTS; ++tau) {
+      if constexpr (kTile) break;
       if (!Full && tau >= nts) break;
       i32x4_t chi[2], clo[2];
 #pragma unroll
@@ -864,7 +921,12 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
 #pragma unroll
       for (int tau = 0; tau < NTS; ++tau) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pk[tau][i] = requant4<Signed>(acc[i][tau], colsum, 16 * tau + 4 * h, s32);
+        for (int i = 0; i < 4; ++i) {
+          if constexpr (kTile)
+            pk[tau][i] = pkall[p][tau][i];
+          else
+            pk[tau][i] = requant4<Signed>(acc[i][tau], colsum, 16 * tau + 4 * h, s32);
+        }
         transpose_rows4(pk[tau]);
       }
       if constexpr (Mode & 32) {  // diagnostics: contiguous 1 KB per store instruction (timing only, wrong data)
@@ -941,14 +1003,14 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_item_kernel(FusedA
   }
 }
 
-template <bool Signed, int NTS, bool Full, int Mode = 0>
+template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3>
 int launch_i8_item(FusedArgs P, hipStream_t st, size_t min_lds = 0) {
   P.nslabs = (P.NT + NTS - 1) / NTS;
   const size_t lds = std::max<size_t>(static_cast<size_t>(2) * NTS * 2 * 64 * 16 + 4 * 32 * 4, min_lds);
   const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
   BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many items");
-  hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode>), dim3(static_cast<unsigned>(n_items)),
-                     dim3(kThreads), lds, st, P);
+  hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ>),
+                     dim3(static_cast<unsigned>(n_items)), dim3(kThreads), lds, st, P);
   BF_LAUNCHED("beamform_fused_i8_item_kernel");
 }
 
@@ -1248,6 +1310,13 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 32: return bf::launch_i8_item<true, 2, true, 32>(P, st);
       case 64: return bf::launch_i8_item<true, 2, true, 0>(P, st, 60 * 1024);  // occupancy 2 (LDS-limited)
       case 65: return bf::launch_i8_item<true, 2, true, 4>(P, st, 60 * 1024);
+      // layout variants: serial coefficients, pol order, both; 4 waves per SIMD (spills), 3 (the product's bound)
+      case 1024: return bf::launch_i8_item<true, 2, true, 1024>(P, st);
+      case 2048: return bf::launch_i8_item<true, 2, true, 2048>(P, st);
+      case 3072: return bf::launch_i8_item<true, 2, true, 3072>(P, st);
+      case 4096: return bf::launch_i8_item<true, 2, true, 0, 4>(P, st);
+      case 4096 + 3072: return bf::launch_i8_item<true, 2, true, 3072, 4>(P, st);
+      case 4096 + 2048: return bf::launch_i8_item<true, 2, true, 2048, 4>(P, st);
       default: bf::set_error("bad mode"); return BF_ERR_ARG;
     }
   }

@@ -42,6 +42,25 @@ __device__ __forceinline__ int coef8_byte(int k, int cl, int nts, int limb) {
   return ((((s * nts + tau) * 2 + limb) * 64) + row + 16 * h) * 16 + j;
 }
 
+// The integer contract's requantisation q = clamp(rne(f32(y) * s), +-127), as the low byte of a float's bits:
+// v = RN(RN(f32(y) * s) + 1.5 * 2^23) carries rne(f32(y) * s) in its low mantissa bits whenever |f32(y) * s| < 2^22
+// (the add lands in [2^23, 2^24), where the float spacing is 1, and the magic constant is even, so the add rounds
+// half to even), and v_med3 against 1.5 * 2^23 +- 127 clamps every larger value to the right end.  The low byte of
+// the clamped bits is then q in two's complement: 3 VALU + a quarter of a pack per value, instead of
+// rint + clamp + float->int + shift/or (7).
+__device__ __forceinline__ uint32_t requant_bits(int y, float s) {
+  constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
+  const float v = __fadd_rn(__fmul_rn(static_cast<float>(y), s), kMagic);
+  return __float_as_uint(__builtin_amdgcn_fmed3f(v, kMagic - 127.0f, kMagic + 127.0f));
+}
+
+// [a.b0, b.b0, c.b0, d.b0]: three v_perm_b32
+__device__ __forceinline__ uint32_t pack_low_bytes(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t ab = __builtin_amdgcn_perm(b, a, 0x0c0c0400u);
+  const uint32_t cd = __builtin_amdgcn_perm(d, c, 0x0c0c0400u);
+  return __builtin_amdgcn_perm(cd, ab, 0x05040100u);
+}
+
 // 4x4 transpose over (lane group h = lane >> 4, register i): afterwards lane group h holds v[i] = old v[h] of lane
 // group i.  Two stages of 2x2 block swaps (rows {0,1}<->{2,3}, then odd<->even rows); all 64 lanes must be active.
 __device__ __forceinline__ void transpose_rows4(uint32_t (&v)[4]) {

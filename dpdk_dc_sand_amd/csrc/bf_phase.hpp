@@ -189,8 +189,10 @@ __device__ __forceinline__ void q14_exact(float4 dv, double ch, double ctot, dou
 
 // N coefficients per lane: fast for all, then an exact pass per flagged coefficient (a wave runs as many exact
 // passes as its most-flagged lane has flags: usually none).  valid[j] false -> W = 0.  FastFirst = false is the
-// exact-only form (diagnostics / ablation).
-template <int N, bool FastFirst = true>
+// exact-only form (diagnostics / ablation).  Serial = true evaluates the N fast phasors one after another
+// (a scheduling barrier between them): less instruction-level parallelism, but the float64 temporaries of only one
+// phasor are live, which is what lets a kernel whose voltage loads are in flight meanwhile fit more waves.
+template <int N, bool FastFirst = true, bool Serial = false>
 __device__ __forceinline__ void q14_coeffs(const float4 (&dv)[N], const float (&g)[N], const bool (&valid)[N],
                                            double ch, double ctot, double ts, double k, double dt, const float* gain,
                                            int (&wc)[N], int (&ws)[N]) {
@@ -206,6 +208,7 @@ __device__ __forceinline__ void q14_coeffs(const float4 (&dv)[N], const float (&
     } else {
       flagged |= 1u << j;
     }
+    if constexpr (Serial) __builtin_amdgcn_sched_barrier(0);
   }
   while (flagged) {
     const int j = __builtin_ctz(flagged);

@@ -259,16 +259,14 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(F
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            uint32_t packed = 0;
+            uint32_t qb[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               int y = (hi[p][i][t][r] << 8) + lo[p][i][t][r];
               if constexpr (!Signed) y += corr[t][r];
-              float v = __builtin_rintf(static_cast<float>(y) * s32);
-              v = fminf(fmaxf(v, -127.0f), 127.0f);
-              packed |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(v)))) << (8 * r);
+              qb[r] = requant_bits(y, s32);
             }
-            pk[t][i] = packed;
+            pk[t][i] = pack_low_bytes(qb[0], qb[1], qb[2], qb[3]);
           }
         const size_t prow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T);
         if (full) {
