@@ -8,6 +8,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -28,10 +29,13 @@ CONFIGS = {
 }
 
 
-def timeit(queue, fn, reps):
-    for _ in range(2):
-        fn()
-    queue.finish()
+def timeit(queue, fn, reps, settle_s=0.2):
+    # untimed clock settle first: the first ~30 ms of load run up to 35 % slower (profiles/r1_v6_clock_ramp.txt)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < settle_s:
+        for _ in range(4):
+            fn()
+        queue.finish()
     e0, e1 = accel.Event(), accel.Event()
     e0.record(queue)
     for _ in range(reps):
