@@ -118,59 +118,57 @@ __device__ __forceinline__ double steering_coeff_fast(float4 dv, double chc, dou
 
 // ---- Q14 phasors of the integer (int8-beam) path ----------------------------------------------------------------
 // Contract (oracle fused_beamform_int8): W = (rint(2^14 re), rint(2^14 im)) of the EXACT phasor (steering_coeff,
-// then the optional gain), ties to even.  q14_fast evaluates the phasor to ~1e-10 instead: float64 rotation without
-// divisions, Cody-Waite reduction, cos/sin with the leading Taylor terms in float64 and the tails (< 4e-4) in
-// float32, so |v - cos(rot_exact)| <= 2.4e-10 (tools/probes/q14_fast_check.c: 2e7 arguments, delays up to 2e5
+// then the optional gain), ties to even.  q14_fast evaluates cos/sin of the reduced angle to ~1e-11 instead:
+// float64 rotation without divisions, two-term Cody-Waite reduction, the fdlibm kernels truncated to five terms
+// in plain float64 Horner form (float64 FMA issues at the float32 rate on CDNA4, so no float32 tails and no
+// conversions), |v - cos(rot_exact)| <= 7.5e-12 (tools/probes/q14_fast_check.c: 2e7 arguments, delays up to 2e5
 // samples) < kQ14Eps.  The exact float32 phasor component is then RN32(v -+ eps) -- one of two adjacent floats --
 // and when both give the same Q14 value (after the gain, as the contract applies it) that value IS the contract's.
-// Otherwise (1.6e-5 of the components), or for a NaN / out-of-range argument, q14_fast returns false and the caller
-// re-evaluates that coefficient exactly: bit-exact at little more than the cost of the float32 phasor.
+// Both Q14 decisions are taken on cos r and sin r of the reduced angle; the quadrant swap and signs are applied to
+// the integers afterwards (Q(-v) = -Q(v): RN32, the gain product and rint are all odd).  Otherwise (1.6e-5 of the
+// components), or for a NaN / out-of-range argument, q14_fast returns false and the caller re-evaluates that
+// coefficient exactly: bit-exact at little more than the cost of a float32 phasor.
 constexpr double kQ14Eps = 5e-10;
 constexpr float kQ14MaxMag = 2e5f;  // |tau'| (ch + Ctot/2) |K| + |phi'| bound of the error analysis above
 
-__device__ __forceinline__ int q14_pair(double v, float g, bool gained, bool* ok) {
-  float a = static_cast<float>(v - kQ14Eps), b = static_cast<float>(v + kQ14Eps);
-  if (gained) {
-    a = __fmul_rn(a, g);
-    b = __fmul_rn(b, g);
-  }
-  const int qa = static_cast<int>(__builtin_rintf(a * 16384.0f)), qb = static_cast<int>(__builtin_rintf(b * 16384.0f));
+// gq = gain * 2^14 (2^14 without gains): RN32(a * g) * 2^14 == RN32(a * gq) (a power-of-two scale commutes with
+// rounding), so the contract's gain product and the Q14 scaling are one multiply.
+__device__ __forceinline__ int q14_pair(double v, float gq, bool* ok) {
+  const float a = static_cast<float>(v - kQ14Eps), b = static_cast<float>(v + kQ14Eps);
+  const float qa = __builtin_rintf(__fmul_rn(a, gq)), qb = __builtin_rintf(__fmul_rn(b, gq));
   *ok = *ok && qa == qb;
-  return qa;
+  return static_cast<int>(qa);
 }
 
-// uk = (ch + Ctot/2) * |K| (uniform per item), for the range check.
-__device__ __forceinline__ bool q14_fast(float4 dv, double chc, double k, double dt, float uk, float g, bool gained,
-                                         int* wc, int* ws) {
-  double tau = static_cast<double>(dv.x);
-  double phi = static_cast<double>(dv.z);
-  if (dt != 0.0) {
-    tau = fma(static_cast<double>(dv.y), dt, tau);
-    phi = fma(static_cast<double>(dv.w), dt, phi);
-  }
+// The truncated fdlibm coefficients (cos C5..C1, -1/2; sin S5..S1) as device memory, not literals: loaded once into
+// SGRPs by s_load, each Horner step is then one VOP3 v_fma_f64 with an SGPR operand, where literal constants made
+// the compiler rematerialise every addend with two v_mov_b32 per step (21 of ~96 VALU per phasor).
+__constant__ double kQ14Poly[11] = {2.08757232129817482790e-09,  -2.75573143513906633035e-07, 2.48015872894767294178e-05,
+                                    -1.38888888888741095749e-03, 4.16666666666666019037e-02,  -2.50507602534068634195e-08,
+                                    2.75573137070700676789e-06,  -1.98412698298579493134e-04, 8.33333333332248946124e-03,
+                                    -1.66666666666666324348e-01, 0.63661977236758138};
+
+// uk = (ch + Ctot/2) * |K| (uniform per item), for the range check.  The rates are applied unconditionally: at
+// dt == 0 they add exact zeros (a non-finite rate makes the range check fail, and the exact path ignores rates).
+__device__ __forceinline__ bool q14_fast(float4 dv, double chc, double k, double dt, float uk, float gq, int* wc,
+                                         int* ws) {
+  const double tau = fma(static_cast<double>(dv.y), dt, static_cast<double>(dv.x));
+  const double phi = fma(static_cast<double>(dv.w), dt, static_cast<double>(dv.z));
+  const double* c = kQ14Poly;
   const double rot = fma(tau * chc, k, phi);
-  const double n = rint(rot * 0.63661977236758138);  // 2 / pi
+  const double n = rint(rot * c[10]);  // 2 / pi
   double r = fma(-n, 1.5707963267948966e+00, rot);
   r = fma(-n, 6.123233995736766e-17, r);
   const double z = r * r;
-  const float zf = static_cast<float>(z);
-  // cos r = 1 - z/2 + z^2/24 - z^3 (1/720 - z/40320 + z^2/3628800 - z^3/479001600)
-  const float tc = zf * zf * zf *
-                   fmaf(fmaf(fmaf(2.0876757e-09f, zf, -2.7557319e-07f), zf, 2.4801587e-05f), zf, -1.3888889e-03f);
-  const double cz = fma(z * z, 4.1666666666666664e-02, fma(z, -0.5, 1.0)) + static_cast<double>(tc);
-  // sin r = r - r z/6 + r z^2/120 - r z^3 (1/5040 - z/362880 + z^2/39916800 - z^3/6227020800)
-  const double rz = r * z, rz2 = rz * z;
-  const float tsn = static_cast<float>(rz2) * zf *
-                    fmaf(fmaf(fmaf(-1.6059044e-10f, zf, 2.5052108e-08f), zf, -2.7557319e-06f), zf, 1.9841270e-04f);
-  const double sz = fma(rz2, 8.3333333333333332e-03, fma(rz, -1.6666666666666666e-01, r)) - static_cast<double>(tsn);
-  const int q = static_cast<int>(static_cast<long long>(n) & 3);
-  const double s0 = (q & 1) ? cz : sz, c0 = (q & 1) ? sz : cz;
-  const double cv = ((q + 1) & 2) ? -c0 : c0;
-  const double sv = (q & 2) ? -s0 : s0;
+  const double cz = fma(z, fma(z, fma(z, fma(z, fma(z, fma(z, c[0], c[1]), c[2]), c[3]), c[4]), -0.5), 1.0);
+  const double sz = fma(r * z, fma(z, fma(z, fma(z, fma(z, c[5], c[6]), c[7]), c[8]), c[9]), r);
   const float mag = fabsf(static_cast<float>(tau)) * uk + fabsf(static_cast<float>(phi));
   bool ok = mag < kQ14MaxMag;  // false for NaN too
-  *wc = q14_pair(cv, g, gained, &ok);
-  *ws = q14_pair(sv, g, gained, &ok);
+  const int qc = q14_pair(cz, gq, &ok), qs = q14_pair(sz, gq, &ok);
+  const int q = __double2int_rn(n) & 3;  // saturating conversion; any garbage is flagged by the range check
+  const int s0 = (q & 1) ? qc : qs, c0 = (q & 1) ? qs : qc;
+  *wc = ((q + 1) & 2) ? -c0 : c0;
+  *ws = (q & 2) ? -s0 : s0;
   return ok;
 }
 
@@ -204,7 +202,7 @@ __device__ __forceinline__ void q14_coeffs(const float4 (&dv)[N], const float (&
     wc[j] = ws[j] = 0;
     if (!valid[j]) continue;
     if constexpr (FastFirst) {
-      if (!q14_fast(dv[j], chc, k, dt, uk, g[j], gain != nullptr, &wc[j], &ws[j])) flagged |= 1u << j;
+      if (!q14_fast(dv[j], chc, k, dt, uk, g[j] * 16384.0f, &wc[j], &ws[j])) flagged |= 1u << j;
     } else {
       flagged |= 1u << j;
     }

@@ -1,5 +1,5 @@
 // Host probe for the integer path's fast Q14 phasor (bf_phase.hpp q14_fast): float64 rotation without divisions,
-// Cody-Waite reduction, cos/sin with the leading Taylor terms in float64 and the tails in float32.  Measures
+// Cody-Waite reduction, truncated fdlibm cos/sin kernels in float64.  Measures
 // max |fast - cos(rot_exact)| (rot_exact = steering_rotation's reference-order float64 phase, libm cos/sin), and
 // checks the decision rule: a = RN32(v - eps), b = RN32(v + eps); unflagged iff rint(2^14 a) == rint(2^14 b),
 // which must then equal rint(2^14 RN32(cos(rot_exact))).
@@ -26,28 +26,25 @@ static double rot_exact(float tau_f, float rate_f, float phi_f, float prate_f, d
   return initial - centre;
 }
 
-// the fast phasor, returning float64 cos/sin approximations (the device code's operation order)
+// the fast phasor, returning float64 cos/sin approximations (the device code's operation order): float64 rotation
+// without divisions, two-term Cody-Waite reduction, truncated fdlibm kernels (sin: S1..S5, cos: C1..C5) in plain
+// float64 Horner form (bf_phase.hpp q14_fast)
 static void fast_phasor(float tau_f, float rate_f, float phi_f, float prate_f, double chc, double k, double dt,
                         double* c, double* s) {
-  double tau = tau_f, phi = phi_f;
-  if (dt != 0.0) { tau = fma((double)rate_f, dt, tau); phi = fma((double)prate_f, dt, phi); }
+  const double tau = fma((double)rate_f, dt, (double)tau_f), phi = fma((double)prate_f, dt, (double)phi_f);
   const double rot = fma(tau * chc, k, phi);
   const double n = rint(rot * 0.63661977236758138);
   double r = fma(-n, 1.5707963267948966e+00, rot);
   r = fma(-n, 6.123233995736766e-17, r);
   const double z = r * r;
-  const float zf = (float)z;
-  // cos r = 1 - z/2 + z^2/24 - z^3 (1/720 - z/40320 + z^2/3628800 - z^3/479001600)
-  const double z2 = z * z;
-  const float tc = zf * zf * zf * fmaf(fmaf(fmaf(2.0876757e-09f, zf, -2.7557319e-07f), zf, 2.4801587e-05f), zf,
-                                       -1.3888889e-03f);
-  const double cz = fma(z2, 4.1666666666666664e-02, fma(z, -0.5, 1.0)) + (double)tc;
-  // sin r = r - r z/6 + r z^2/120 - r z^3 (1/5040 - z/362880 + z^2/39916800 - z^3/6227020800)
-  const double rz = r * z, rz2 = rz * z;
-  const float ts = (float)rz2 * zf * fmaf(fmaf(fmaf(-1.6059044e-10f, zf, 2.5052108e-08f), zf, -2.7557319e-06f), zf,
-                                          1.9841270e-04f);
-  const double sz = fma(rz2, 8.3333333333333332e-03, fma(rz, -1.6666666666666666e-01, r)) - (double)ts;
-  const int q = (int)((long long)n & 3);
+  const double cz = fma(z, fma(z, fma(z, fma(z, fma(z, fma(z, 2.08757232129817482790e-09, -2.75573143513906633035e-07),
+                                                    2.48015872894767294178e-05), -1.38888888888741095749e-03),
+                                      4.16666666666666019037e-02), -0.5), 1.0);
+  const double sp = fma(z, fma(z, fma(z, fma(z, -2.50507602534068634195e-08, 2.75573137070700676789e-06),
+                                      -1.98412698298579493134e-04), 8.33333333332248946124e-03),
+                        -1.66666666666666324348e-01);
+  const double sz = fma(r * z, sp, r);
+  const int q = (int)n & 3;
   const double s0 = (q & 1) ? cz : sz, c0 = (q & 1) ? sz : cz;
   *c = ((q + 1) & 2) ? -c0 : c0;
   *s = (q & 2) ? -s0 : s0;
