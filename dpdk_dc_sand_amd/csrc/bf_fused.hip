@@ -37,6 +37,8 @@ constexpr int kCachedLoad = 128, kNtStore = 256;
 // restores the pol-outermost contraction of full slabs (the product runs sample-row-outermost with immediate
 // requantisation: -1.3 % at 3 waves per SIMD).
 constexpr int kSerialCoef = 1024, kPolOrder = 2048;
+// Cache-policy variants of the integer item kernel (which streams with non-temporal loads and stores).
+constexpr int kI8PlainStore = 8192, kI8PlainLoad = 16384;
 
 // One group of 4 k-steps: 16 x 16-byte loads per lane, all UNCONDITIONAL: out-of-range antennas (a >= A) read
 // antenna A-1 and meet zero coefficient rows, out-of-range time quads read the last quad and are never stored,
@@ -682,6 +684,14 @@ __device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* cols
 // fragments, 8 i8 MFMAs per (sample, tile), requantise, 4-byte stores.
 // Mode (diagnostics only): kSkipCoef / kSkipMfma / kSkipStore / kSkipLoad as the float item kernel; 16 = fast
 // (f32 sincos) coefficients only (inexact); 128 = exact coefficients only (no fast attempt).
+template <int Mode>
+__device__ __forceinline__ void st_i8(u32x4_t v, u32x4_t* p) {
+  if constexpr (Mode & kI8PlainStore)
+    *p = v;
+  else
+    __builtin_nontemporal_store(v, p);
+}
+
 template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3>
 __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
@@ -722,8 +732,8 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
     for (int q = 0; q < 8; ++q) {
       int a = 32 * ss + 8 * h + q;
       a = a < P.A ? a : P.A - 1;
-      const u32x4_t v = __builtin_nontemporal_load(
-          reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a) * ant_stride + tqc * 16u));
+      const u32x4_t* src = reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a) * ant_stride + tqc * 16u);
+      const u32x4_t v = (Mode & kI8PlainLoad) ? *src : __builtin_nontemporal_load(src);
       d[ss][q][0] = v[0];
       d[ss][q][1] = v[1];
       d[ss][q][2] = v[2];
@@ -958,7 +968,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
             }
           }
           if (64 * wave + r < P.T)
-            __builtin_nontemporal_store(u32x4_t{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4_t*>(o + 1024 * si));
+            st_i8<Mode>(u32x4_t{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4_t*>(o + 1024 * si));
         }
         continue;
       }
@@ -967,8 +977,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
         int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow * M2 + 16 * tau0;
 #pragma unroll
         for (int tau = 0; tau < NTS; ++tau)
-          __builtin_nontemporal_store(u32x4_t{pk[tau][0], pk[tau][1], pk[tau][2], pk[tau][3]},
-                                      reinterpret_cast<u32x4_t*>(o + 16 * tau));
+          st_i8<Mode>(u32x4_t{pk[tau][0], pk[tau][1], pk[tau][2], pk[tau][3]}, reinterpret_cast<u32x4_t*>(o + 16 * tau));
       }
       continue;
     }
@@ -1317,6 +1326,9 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 4096: return bf::launch_i8_item<true, 2, true, 0, 4>(P, st);
       case 4096 + 3072: return bf::launch_i8_item<true, 2, true, 3072, 4>(P, st);
       case 4096 + 2048: return bf::launch_i8_item<true, 2, true, 2048, 4>(P, st);
+      case 8192: return bf::launch_i8_item<true, 2, true, 8192>(P, st);
+      case 16384: return bf::launch_i8_item<true, 2, true, 16384>(P, st);
+      case 8192 + 16384: return bf::launch_i8_item<true, 2, true, 8192 + 16384>(P, st);
       default: bf::set_error("bad mode"); return BF_ERR_ARG;
     }
   }

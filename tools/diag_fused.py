@@ -87,7 +87,8 @@ if "w8" in _os.environ.get("DIAG_KERNELS", ""):
 names_i8 = {0: "full (fast+fixup coef, occ 3)", 128: "exact-only coef", 16: "fast coef (inexact)", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store",
             5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
             65: "occ 2, no-store", 1024: "serial coef", 2048: "pol order", 3072: "serial+pol order",
-            4096: "occ4 (spills)", 7168: "occ4 serial+pol", 6144: "occ4 pol order"}
+            4096: "occ4 (spills)", 7168: "occ4 serial+pol", 6144: "occ4 pol order",
+            8192: "plain stores", 16384: "plain loads", 24576: "plain loads+stores"}
 alg_i8 = nin + nout // 4
 for kbase, kname in ((0, "pipe"), (32, "item"), (512, "i8")):
     if _os.environ.get("DIAG_KERNELS", "item,pipe,i8").find(kname) < 0:
