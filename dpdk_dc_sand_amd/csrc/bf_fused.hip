@@ -679,11 +679,6 @@ __device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* cols
 }
 
 
-// Item form of the integer kernel (A <= 64, T <= 256): one (slab, b, c) per workgroup, issue order delay model ->
-// voltages (16 x 16 B per lane) -> exact coefficients + Q14 limbs under them -> barrier -> per pol: v_perm
-// fragments, 8 i8 MFMAs per (sample, tile), requantise, 4-byte stores.
-// Mode (diagnostics only): kSkipCoef / kSkipMfma / kSkipStore / kSkipLoad as the float item kernel; 16 = fast
-// (f32 sincos) coefficients only (inexact); 128 = exact coefficients only (no fast attempt).
 template <int Mode>
 __device__ __forceinline__ void st_i8(u32x4_t v, u32x4_t* p) {
   if constexpr (Mode & kI8PlainStore)
@@ -692,6 +687,164 @@ __device__ __forceinline__ void st_i8(u32x4_t v, u32x4_t* p) {
     __builtin_nontemporal_store(v, p);
 }
 
+// The item's Q14 coefficient table: exact-contract phasors of this thread's (antenna, beam) pairs (fast + fixup) ->
+// hi/lo int8 limb fragments in LDS (coef8_byte layout) + the per-wave column sums of the unsigned correction.
+// Mode (diagnostics): kSkipCoef synthetic values, 16 float32 phasors only (inexact), 128 exact only, kSerialCoef.
+template <bool Signed, int NTS, int Mode>
+__device__ __forceinline__ void i8_coef_phase(int8_t* lb, int* colsum, const CoefPrefetch<NTS>& cp, const FusedArgs& P,
+                                              int b, int c, int tau0, int nts, int S8, int tid, int lane, int wave) {
+  const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+  const int nbeam = nts * 8;
+  const int npairs = S8 * 32 * nbeam;
+  const double ch = static_cast<double>(P.base_ch + c);
+  // this thread's contributions to columns 2ml, 2ml+1: ml = tid % nbeam for every pair it owns (256 % nbeam == 0)
+  int cs0 = 0, cs1 = 0;
+  constexpr int NP = CoefPrefetch<NTS>::kMaxPairs;
+  bool valid[NP];
+  int wc[NP], ws[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int e = tid + j * kThreads;
+    const int a = e / nbeam, m = tau0 * 8 + (e - a * nbeam);
+    valid[j] = e < npairs && a < P.A && m < P.M;
+  }
+  if constexpr (Mode & kSkipCoef) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      wc[j] = 8192 + 16 * j + tid;
+      ws[j] = 4096 - 16 * j;
+    }
+  } else if constexpr (Mode & 16) {  // diagnostics: float32 phasors only (not the contract)
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      float re, im;
+      steering_coeff_fast(cp.dv[j], ch - P.ctot / 2.0, P.k, dt, &re, &im);
+      wc[j] = static_cast<int>(__builtin_rintf(re * 16384.0f));
+      ws[j] = static_cast<int>(__builtin_rintf(im * 16384.0f));
+    }
+  } else {
+    q14_coeffs<NP, !(Mode & 128), (Mode & kSerialCoef) != 0>(cp.dv, cp.g, valid, ch, P.ctot, P.ts, P.k, dt,
+                                                               P.gain, wc, ws);
+  }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int e = tid + j * kThreads;
+    if (e >= npairs) break;
+    const int a = e / nbeam, ml = e - a * nbeam;
+    const int Wc = wc[j], Ws = ws[j];
+    const int cl = 2 * ml;
+    // (k, k + 1) = (2a, 2a + 1) are adjacent bytes of one column: one 16-bit write per (column, limb)
+    const int col_w[2][2] = {{Wc, -Ws}, {Ws, Wc}};  // [column cl + ec][k = 2a + f]
+#pragma unroll
+    for (int ec = 0; ec < 2; ++ec) {
+      int h2[2], l2[2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        l2[f] = ((col_w[ec][f] + 128) & 255) - 128;
+        h2[f] = (col_w[ec][f] - l2[f]) >> 8;
+      }
+      *reinterpret_cast<uint16_t*>(lb + coef8_byte(2 * a, cl + ec, nts, 0)) =
+          static_cast<uint16_t>((h2[0] & 255) | ((h2[1] & 255) << 8));
+      *reinterpret_cast<uint16_t*>(lb + coef8_byte(2 * a, cl + ec, nts, 1)) =
+          static_cast<uint16_t>((l2[0] & 255) | ((l2[1] & 255) << 8));
+    }
+    cs0 += Wc - Ws;  // column 2m:   W[2a][2m] + W[2a+1][2m]
+    cs1 += Ws + Wc;  // column 2m+1: W[2a][2m+1] + W[2a+1][2m+1]
+  }
+  if constexpr (!Signed) {
+    // nbeam (8 or 16) divides 64: lanes with equal lane % nbeam share ml; reduce them, one partial per wave
+    for (int off = nbeam; off < 64; off <<= 1) {
+      cs0 += __shfl_xor(cs0, off);
+      cs1 += __shfl_xor(cs1, off);
+    }
+    if (lane < nbeam) {
+      colsum[wave * 32 + 2 * lane] = cs0;
+      colsum[wave * 32 + 2 * lane + 1] = cs1;
+    }
+  }
+}
+
+// Full-slab contraction: sample row i outermost, both pols inside, each 4-MFMA chain (hi limbs, << 8, lo limbs)
+// requantised at once into packed int8 columns pkall[p][tau][i] (lane (tl, h): row 4 tq + i, columns 16 tau + 4 h ..).
+template <bool Signed, int NTS>
+__device__ __forceinline__ void i8_contract_rows(const int4* fr, const uint32_t (&d)[2][8][4], const int* colsum,
+                                                 float s32, int S8, int lane, int h, uint32_t (&pkall)[2][NTS][4]) {
+  i32x4_t chi[2][NTS], clo[2][NTS];
+#pragma unroll
+  for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+    for (int tau = 0; tau < NTS; ++tau) {
+      if (ss < S8) {
+        const int4 x0 = fr[(((ss * NTS + tau) * 2 + 0) * 64) + lane];
+        const int4 x1 = fr[(((ss * NTS + tau) * 2 + 1) * 64) + lane];
+        chi[ss][tau] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
+        clo[ss][tau] = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+      } else {
+        chi[ss][tau] = clo[ss][tau] = i32x4_t{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const uint32_t sel = p ? kSelP1 : kSelP0;
+      i32x4_t f[2];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        uint32_t w[4];
+#pragma unroll
+        for (int m2 = 0; m2 < 4; ++m2) {
+          uint32_t lo = d[ss][2 * m2][i], hi = d[ss][2 * m2 + 1][i];
+          if constexpr (!Signed) {
+            lo ^= 0x80808080u;
+            hi ^= 0x80808080u;
+          }
+          w[m2] = __builtin_amdgcn_perm(hi, lo, sel);
+        }
+        f[ss] = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]),
+                        static_cast<int>(w[3])};
+      }
+#pragma unroll
+      for (int tau = 0; tau < NTS; ++tau) {
+        i32x4_t t = mfma_i8(chi[0][tau], f[0], i32x4_t{0, 0, 0, 0});
+        t = mfma_i8(chi[1][tau], f[1], t);
+        t = t << 8;
+        t = mfma_i8(clo[0][tau], f[0], t);
+        t = mfma_i8(clo[1][tau], f[1], t);
+        pkall[p][tau][i] = requant4<Signed>(t, colsum, 16 * tau + 4 * h, s32);
+      }
+    }
+  }
+}
+
+// A wave's 64 output rows of a full-width slab (M2 == 16 NTS) are one contiguous 1-2 KiB block: after the row
+// transpose lane (tl, h) holds row 4 tl + h; ds_bpermute the row-per-lane chunks so that store instruction si
+// writes bytes [1024 si, 1024 si + 1024) of the block.  rows = valid rows of the block (T - 64 wave).
+template <int NTS, int Mode>
+__device__ __forceinline__ void i8_store_block(const uint32_t (&pk)[NTS][4], int8_t* block, int lane, int rows) {
+#pragma unroll
+  for (int si = 0; si < NTS; ++si) {
+    const int f = 64 * si + lane;  // flat 16-B chunk of the block
+    const int r = f / NTS, ch = f % NTS;
+    const int src = 4 * ((r >> 2) + 16 * (r & 3));  // lane (tl, h) = (r >> 2, r & 3) holds row r
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      w[j] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(pk[0][j])));
+      if constexpr (NTS == 2) {
+        const uint32_t w1 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(pk[1][j])));
+        w[j] = ch ? w1 : w[j];
+      }
+    }
+    if (r < rows) st_i8<Mode>(u32x4_t{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4_t*>(block + 16 * lane + 1024 * si));
+  }
+}
+
+// Item form of the integer kernel (A <= 64, T <= 256): one (slab, b, c) per workgroup, issue order delay model ->
+// voltages (16 x 16 B per lane) -> exact coefficients + Q14 limbs under them -> barrier -> per pol: v_perm
+// fragments, 8 i8 MFMAs per (sample, tile), requantise, 4-byte stores.
+// Mode (diagnostics only): kSkipCoef / kSkipMfma / kSkipStore / kSkipLoad as the float item kernel; 16 = fast
+// (f32 sincos) coefficients only (inexact); 128 = exact coefficients only (no fast attempt).
 template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3>
 __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
@@ -741,77 +894,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
     }
   }
   __builtin_amdgcn_sched_barrier(0);
-  {
-    const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
-    const int nbeam = nts * 8;
-    const int npairs = S8 * 32 * nbeam;
-    const double ch = static_cast<double>(P.base_ch + c);
-    // this thread's contributions to columns 2ml, 2ml+1: ml = tid % nbeam for every pair it owns (256 % nbeam == 0)
-    int cs0 = 0, cs1 = 0;
-    constexpr int NP = CoefPrefetch<NTS>::kMaxPairs;
-    bool valid[NP];
-    int wc[NP], ws[NP];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int e = tid + j * kThreads;
-      const int a = e / nbeam, m = tau0 * 8 + (e - a * nbeam);
-      valid[j] = e < npairs && a < P.A && m < P.M;
-    }
-    if constexpr (Mode & kSkipCoef) {
-#pragma unroll
-      for (int j = 0; j < NP; ++j) {
-        wc[j] = 8192 + 16 * j + tid;
-        ws[j] = 4096 - 16 * j;
-      }
-    } else if constexpr (Mode & 16) {  // diagnostics: float32 phasors only (not the contract)
-#pragma unroll
-      for (int j = 0; j < NP; ++j) {
-        float re, im;
-        steering_coeff_fast(cp.dv[j], ch - P.ctot / 2.0, P.k, dt, &re, &im);
-        wc[j] = static_cast<int>(__builtin_rintf(re * 16384.0f));
-        ws[j] = static_cast<int>(__builtin_rintf(im * 16384.0f));
-      }
-    } else {
-      q14_coeffs<NP, !(Mode & 128), (Mode & kSerialCoef) != 0>(cp.dv, cp.g, valid, ch, P.ctot, P.ts, P.k, dt,
-                                                                 P.gain, wc, ws);
-    }
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int e = tid + j * kThreads;
-      if (e >= npairs) break;
-      const int a = e / nbeam, ml = e - a * nbeam;
-      const int Wc = wc[j], Ws = ws[j];
-      const int cl = 2 * ml;
-      // (k, k + 1) = (2a, 2a + 1) are adjacent bytes of one column: one 16-bit write per (column, limb)
-      const int col_w[2][2] = {{Wc, -Ws}, {Ws, Wc}};  // [column cl + ec][k = 2a + f]
-#pragma unroll
-      for (int ec = 0; ec < 2; ++ec) {
-        int h2[2], l2[2];
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          l2[f] = ((col_w[ec][f] + 128) & 255) - 128;
-          h2[f] = (col_w[ec][f] - l2[f]) >> 8;
-        }
-        *reinterpret_cast<uint16_t*>(lb + coef8_byte(2 * a, cl + ec, nts, 0)) =
-            static_cast<uint16_t>((h2[0] & 255) | ((h2[1] & 255) << 8));
-        *reinterpret_cast<uint16_t*>(lb + coef8_byte(2 * a, cl + ec, nts, 1)) =
-            static_cast<uint16_t>((l2[0] & 255) | ((l2[1] & 255) << 8));
-      }
-      cs0 += Wc - Ws;  // column 2m:   W[2a][2m] + W[2a+1][2m]
-      cs1 += Ws + Wc;  // column 2m+1: W[2a][2m+1] + W[2a+1][2m+1]
-    }
-    if constexpr (!Signed) {
-      // nbeam (8 or 16) divides 64: lanes with equal lane % nbeam share ml; reduce them, one partial per wave
-      for (int off = nbeam; off < 64; off <<= 1) {
-        cs0 += __shfl_xor(cs0, off);
-        cs1 += __shfl_xor(cs1, off);
-      }
-      if (lane < nbeam) {
-        colsum[wave * 32 + 2 * lane] = cs0;
-        colsum[wave * 32 + 2 * lane + 1] = cs1;
-      }
-    }
-  }
+  i8_coef_phase<Signed, NTS, Mode>(lb, colsum, cp, P, b, c, tau0, nts, S8, tid, lane, wave);
   __syncthreads();
   const int4* fr = reinterpret_cast<const int4*>(lds);
   const float s32 = P.out_scale * 0x1p-14f;
@@ -820,54 +903,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
   // packed bytes (16 VGPRs) stay live and the voltage registers of row i die after it.
   constexpr bool kTile = Full && !(Mode & (kSkipMfma | kSkipStore | kSkipLoad | kPolOrder));
   uint32_t pkall[2][NTS][4];
-  if constexpr (kTile) {
-    i32x4_t chi[2][NTS], clo[2][NTS];
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-      for (int tau = 0; tau < NTS; ++tau) {
-        if (ss < S8) {
-          const int4 x0 = fr[(((ss * NTS + tau) * 2 + 0) * 64) + lane];
-          const int4 x1 = fr[(((ss * NTS + tau) * 2 + 1) * 64) + lane];
-          chi[ss][tau] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
-          clo[ss][tau] = i32x4_t{x1.x, x1.y, x1.z, x1.w};
-        } else {
-          chi[ss][tau] = clo[ss][tau] = i32x4_t{0, 0, 0, 0};
-        }
-      }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const uint32_t sel = p ? kSelP1 : kSelP0;
-        i32x4_t f[2];
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          uint32_t w[4];
-#pragma unroll
-          for (int m2 = 0; m2 < 4; ++m2) {
-            uint32_t lo = d[ss][2 * m2][i], hi = d[ss][2 * m2 + 1][i];
-            if constexpr (!Signed) {
-              lo ^= 0x80808080u;
-              hi ^= 0x80808080u;
-            }
-            w[m2] = __builtin_amdgcn_perm(hi, lo, sel);
-          }
-          f[ss] = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]),
-                          static_cast<int>(w[3])};
-        }
-#pragma unroll
-        for (int tau = 0; tau < NTS; ++tau) {
-          i32x4_t t = mfma_i8(chi[0][tau], f[0], i32x4_t{0, 0, 0, 0});
-          t = mfma_i8(chi[1][tau], f[1], t);
-          t = t << 8;
-          t = mfma_i8(clo[0][tau], f[0], t);
-          t = mfma_i8(clo[1][tau], f[1], t);
-          pkall[p][tau][i] = requant4<Signed>(t, colsum, 16 * tau + 4 * h, s32);
-        }
-      }
-    }
-  }
+  if constexpr (kTile) i8_contract_rows<Signed, NTS>(fr, d, colsum, s32, S8, lane, h, pkall);
 
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -952,24 +988,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
         // the slab is the whole row, so the wave's 64 rows are one contiguous 1-2 KB block: ds_bpermute the
         // row-per-lane chunks so that store instruction s writes bytes [1024 s, 1024 s + 1024) of it.
         const size_t orow0 = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 64 * wave;
-        int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow0 * M2 + 16 * lane;
-#pragma unroll
-        for (int si = 0; si < NTS; ++si) {
-          const int f = 64 * si + lane;  // flat 16-B chunk of the block
-          const int r = f / NTS, ch = f % NTS;
-          const int src = 4 * ((r >> 2) + 16 * (r & 3));  // lane (tl, h) = (r >> 2, r & 3) holds row r
-          uint32_t w[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            w[j] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(pk[0][j])));
-            if constexpr (NTS == 2) {
-              const uint32_t w1 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(pk[1][j])));
-              w[j] = ch ? w1 : w[j];
-            }
-          }
-          if (64 * wave + r < P.T)
-            st_i8<Mode>(u32x4_t{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4_t*>(o + 1024 * si));
-        }
+        i8_store_block<NTS, Mode>(pk, reinterpret_cast<int8_t*>(P.y) + orow0 * M2, lane, P.T - 64 * wave);
         continue;
       }
       if (tv) {

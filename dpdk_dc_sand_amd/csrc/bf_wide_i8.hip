@@ -26,9 +26,17 @@ __device__ __forceinline__ int w8_step_base(int s, int A) { return min(32 * s, A
 // k-steps of 32 antennas, padded to an even count (ping-pong, see the float wide kernel)
 __host__ __device__ inline int w8_padded_steps(int A) { return 2 * ((((A + 31) >> 5) + 1) / 2); }
 
-template <int Mode>
-__device__ __forceinline__ void w8_load(const uint8_t* __restrict__ base, size_t ant_stride, uint32_t loff, int s,
-                                        int A, uint32_t (&d)[8][4]) {
+// The item's voltages as a buffer resource (gfx9 raw-buffer descriptor word 3): every load is then
+// buffer_load_dwordx4 with the lane offset in a VGPR and the wave-uniform antenna offset in an SGPR -- no per-load
+// 64-bit address arithmetic on the VALU (3 instructions per load, one of them a v_mad_u64_u32, in the pointer form).
+// Needs every offset < 2^31 (the host checks A * C * T * 4); otherwise the pointer form is used.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t w8_rsrc(const uint8_t* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+template <int Mode, bool Buf>
+__device__ __forceinline__ void w8_load(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t rsrc, size_t ant_stride,
+                                        uint32_t loff, int s, int A, uint32_t (&d)[8][4]) {
   const int a0 = w8_step_base(s, A);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -37,7 +45,12 @@ __device__ __forceinline__ void w8_load(const uint8_t* __restrict__ base, size_t
       for (int j = 0; j < 4; ++j) d[q][j] = loff * 0x01010101u + s + q + j;
       continue;
     }
-    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a0 + q) * ant_stride + loff);
+    u32x4_t v;
+    if constexpr (Buf)
+      v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                          rsrc, loff, static_cast<uint32_t>(a0 + q) * static_cast<uint32_t>(ant_stride), 0));
+    else
+      v = *reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a0 + q) * ant_stride + loff);
     d[q][0] = v[0];
     d[q][1] = v[1];
     d[q][2] = v[2];
@@ -88,7 +101,7 @@ __device__ __forceinline__ void w8_contract(const int4* __restrict__ fr, int s, 
 }
 
 // Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads.
-template <bool Signed, int Mode = 0>
+template <bool Signed, int Mode = 0, bool Buf = true>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -111,14 +124,15 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(F
   const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
   const uint32_t hoff = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride);  // < 24 * stride
   const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+  const __amdgpu_buffer_rsrc_t rsrc = w8_rsrc(base);
   int8_t* lb = reinterpret_cast<int8_t*>(lds4);
   int* partial = reinterpret_cast<int*>(lb + static_cast<size_t>(Sp) * 2 * 2 * 64 * 16);  // [4 waves][32 columns]
 
   uint32_t d0[8][4], d1[8][4];
   int chunk = wave;
   uint32_t loff = hoff + static_cast<uint32_t>(min(chunk * 16 + tl, T4 - 1)) * 16u;
-  w8_load<Mode>(base, ant_stride, loff, 0, P.A, d0);
-  w8_load<Mode>(base, ant_stride, loff, 1, P.A, d1);
+  w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, 0, P.A, d0);
+  w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, 1, P.A, d1);
 
   // Q14 limbs of the slab's [[R, I], [-I, R]] blocks for every slot antenna (exact float64 phasors), under the
   // loads.  Pair e -> 4 consecutive slot antennas x beam row ml (ml is fixed per thread: the column sums of the
@@ -230,17 +244,17 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(F
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int t = 0; t < 2; ++t) hi[p][i][t] = lo[p][i][t] = i32x4_t{0, 0, 0, 0};
-    for (int s = 0; s < Sp; s += 2) {  // ping-pong, unconditional clamped prefetch (exact vmcnt, see bf_wide.hip)
-      w8_contract<Signed, Mode>(lds4, s, lane, d0, hi, lo);
-      w8_load<Mode>(base, ant_stride, loff, min(s + 2, Sp - 1), P.A, d0);
-      w8_contract<Signed, Mode>(lds4, s + 1, lane, d1, hi, lo);
-      w8_load<Mode>(base, ant_stride, loff, min(s + 3, Sp - 1), P.A, d1);
-    }
+      for (int s = 0; s < Sp; s += 2) {  // ping-pong, unconditional clamped prefetch (exact vmcnt, see bf_wide.hip)
+        w8_contract<Signed, Mode>(lds4, s, lane, d0, hi, lo);
+        w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, min(s + 2, Sp - 1), P.A, d0);
+        w8_contract<Signed, Mode>(lds4, s + 1, lane, d1, hi, lo);
+        w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, min(s + 3, Sp - 1), P.A, d1);
+      }
     const int next = chunk + 4;
-    if (pass + 1 < npasses) {  // next chunk's first two steps in flight during the stores
+    if (pass + 1 < npasses) {  // next chunk's first steps in flight during the stores
       loff = hoff + static_cast<uint32_t>(min(next * 16 + tl, T4 - 1)) * 16u;
-      w8_load<Mode>(base, ant_stride, loff, 0, P.A, d0);
-      w8_load<Mode>(base, ant_stride, loff, 1, P.A, d1);
+      w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, 0, P.A, d0);
+      w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, 1, P.A, d1);
     }
     if constexpr (Mode & 4) {
       int sum = 0;
@@ -310,8 +324,21 @@ int launch_w8(FusedArgs P, hipStream_t st) {
   const long long items = static_cast<long long>(P.B) * P.C;
   const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
-  hipLaunchKernelGGL((beamform_fused_i8_wide_kernel<Signed, Mode>), dim3(static_cast<unsigned>(grid)),
-                     dim3(kW8Threads), lds, st, P);
+  // Buffer-resource loads (BF_W8_BUFFER=1, signed samples, in-item offsets below 2^31): the contraction alone runs
+  // faster with them (no-coef/no-store 367 vs 394 us), the full kernel slower (609 vs 592 us, interleaved A/B,
+  // profiles/r1_v7_w8_buffer_ab.txt), so the pointer form is the default.
+  const char* bo = getenv("BF_W8_BUFFER");
+  const bool buf = Signed && static_cast<unsigned long long>(P.A) * P.C * P.T * 4 < (1ull << 31) &&
+                   (bo && bo[0] == '1');
+  if constexpr (Signed) {
+    if (buf) {
+      hipLaunchKernelGGL((beamform_fused_i8_wide_kernel<Signed, Mode, true>), dim3(static_cast<unsigned>(grid)),
+                         dim3(kW8Threads), lds, st, P);
+      BF_LAUNCHED("beamform_fused_i8_wide_kernel");
+    }
+  }
+    hipLaunchKernelGGL((beamform_fused_i8_wide_kernel<Signed, Mode, false>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW8Threads), lds, st, P);
   BF_LAUNCHED("beamform_fused_i8_wide_kernel");
 }
 

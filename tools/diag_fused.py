@@ -80,6 +80,16 @@ if "w8" in _os.environ.get("DIAG_KERNELS", ""):
         for mode in w8names:
             res[mode].append(timeit(lambda i: lib.bf_diag_w8(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
                                                              B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
+    if _os.environ.get("W8_AB"):  # interleaved A/B of the load form (buffer resource vs pointer), full kernel
+        ab = {"buffer": [], "pointer": []}
+        for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
+            for form, val in (("buffer", "1"), ("pointer", "0")):
+                _os.environ["BF_W8_BUFFER"] = val
+                ab[form].append(timeit(lambda i: lib.bf_diag_w8(0, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
+                                                                B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
+        for form, ts in ab.items():
+            ts = sorted(ts)
+            print(f"  w8 full, {form:7s} loads  median {ts[len(ts) // 2] * 1e6:8.1f} us  min {ts[0] * 1e6:8.1f} us")
     for mode in w8names:
         ts = sorted(res[mode])
         print(f"  w8 mode {mode:2d} {w8names[mode]:18s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "

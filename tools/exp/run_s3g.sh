@@ -1,0 +1,5 @@
+set -o pipefail
+O=gpurun_out/s3g; mkdir -p $O
+export TMPDIR=/tmp
+DIAG_KERNELS=w8 DIAG_ROUNDS=3 DIAG_STREAMS=0 timeout -k 10 400 python -u tools/diag_fused.py 1 4096 256 256 64 > $O/diag_w8.txt 2>&1 || { echo "diag w8 failed"; tail -20 $O/diag_w8.txt; exit 1; }
+cat $O/diag_w8.txt
