@@ -1367,6 +1367,8 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 128: return bf::launch_item<true, false, 2, false, true, 128>(P, st);
       case 256: return bf::launch_item<true, false, 2, false, true, 256>(P, st);
       case 384: return bf::launch_item<true, false, 2, false, true, 384>(P, st);
+      case 64: return bf::launch_item<true, false, 2, false, true, 0, 4>(P, st);  // 4 waves per SIMD bound
+      case 96: return bf::launch_item<true, false, 2, false, true, 0, 3>(P, st);  // 3 waves per SIMD bound
       default: bf::set_error("bad mode"); return BF_ERR_ARG;
     }
   }
