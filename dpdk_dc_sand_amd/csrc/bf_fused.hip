@@ -1010,6 +1010,26 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
       if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[tid] = sum;
       continue;
     }
+    if constexpr (NTS == 1) {
+      if (M2 == 2 || M2 == 4) {
+        // one or two beams (config 2): lane (tl, h = 0) holds every column of rows 4 tq .. 4 tq + 3, which are
+        // 4 M2 contiguous bytes: one 8- or 16-byte store per lane instead of 4 M2 byte stores
+        uint32_t pk[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pk[i] = requant4<Signed>(acc[i][0], colsum, 4 * h, s32);
+        if (h == 0) {
+          const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq;
+          int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow * M2;
+          if (M2 == 2)
+            __builtin_nontemporal_store(u32x2_t{__builtin_amdgcn_perm(pk[1], pk[0], 0x05040100u),
+                                                __builtin_amdgcn_perm(pk[3], pk[2], 0x05040100u)},
+                                        reinterpret_cast<u32x2_t*>(o));
+          else
+            st_i8<Mode>(u32x4_t{pk[0], pk[1], pk[2], pk[3]}, reinterpret_cast<u32x4_t*>(o));
+        }
+        continue;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq + i;

@@ -8,6 +8,7 @@
 namespace bf {
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 
 struct FusedArgs {
   const uint8_t* raw;

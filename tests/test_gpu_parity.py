@@ -316,6 +316,25 @@ def test_fused_int8_bit_exact(context, command_queue, monkeypatch, i8_kernel, A,
         assert np.abs(ref.astype(int)).max() >= 4  # not a trivially zero case
 
 
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("signed", [True, False])
+@pytest.mark.parametrize("A,T", [(64, 256), (61, 256), (64, 144), (19, 64)])
+def test_fused_int8_one_two_beams(context, command_queue, A, T, M, signed):
+    """Config-2-like shapes (one or two beams): the item kernel's packed 8/16-byte row stores, bit-exact."""
+    B, C, Ctot, xeng, bdt = 2, 3, 4096, 2, 256 * 8192 * TS
+    d = random_delays(1, M, A, 11 * A + M)
+    rng = np.random.default_rng(5 * A + T + M)
+    raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8)
+    if signed:
+        raw = raw.view(np.int8)
+    op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=signed,
+                                 out_int8=True, out_scale=1 / 32, batch_dt=bdt).instantiate(command_queue)
+    (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    np.testing.assert_array_equal(q, O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, batch_dt=bdt, scale=1 / 32,
+                                                           signed=signed))
+    assert np.abs(q.astype(int)).max() >= 4
+
+
 def test_fused_int8_float_path_is_requantised_f32(context, command_queue, monkeypatch):
     """Measurement path (BF_FUSED_INT8_FLOAT=1): float beams requantised in-kernel == bf_requant(float beams)."""
     monkeypatch.setenv("BF_FUSED_INT8_FLOAT", "1")
