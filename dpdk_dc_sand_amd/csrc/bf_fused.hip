@@ -218,6 +218,24 @@ template <bool OutI8, int NTS, bool Full, bool Nt = false>
 __device__ __forceinline__ void store_pol(const FusedArgs& P, int b, int c, int p, int tau0, int nts, int tq, int h,
                                           const f32x4 (&acc)[4][NTS]) {
   const int M2 = 2 * P.M;
+  if constexpr (!OutI8 && !Full && NTS == 1) {
+    if (M2 == 2 || M2 == 4) {
+      // one or two beams (config 2): lane (tl, h = 0) holds every column of rows 4 tq .. 4 tq + 3, 4 M2 contiguous
+      // floats: 16-byte stores instead of one 4-byte store per value
+      if (h == 0) {
+        const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq;
+        f32x4* o = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.y) + orow * M2);
+        if (M2 == 2) {
+          o[0] = f32x4{acc[0][0][0], acc[0][0][1], acc[1][0][0], acc[1][0][1]};
+          o[1] = f32x4{acc[2][0][0], acc[2][0][1], acc[3][0][0], acc[3][0][1]};
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = acc[i][0];
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq + i;

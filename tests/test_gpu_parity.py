@@ -320,7 +320,8 @@ def test_fused_int8_bit_exact(context, command_queue, monkeypatch, i8_kernel, A,
 @pytest.mark.parametrize("signed", [True, False])
 @pytest.mark.parametrize("A,T", [(64, 256), (61, 256), (64, 144), (19, 64)])
 def test_fused_int8_one_two_beams(context, command_queue, A, T, M, signed):
-    """Config-2-like shapes (one or two beams): the item kernel's packed 8/16-byte row stores, bit-exact."""
+    """Config-2-like shapes (one or two beams): the item kernels' packed row stores -- int8 bit-exact, f32 within the
+    tolerance."""
     B, C, Ctot, xeng, bdt = 2, 3, 4096, 2, 256 * 8192 * TS
     d = random_delays(1, M, A, 11 * A + M)
     rng = np.random.default_rng(5 * A + T + M)
@@ -333,6 +334,11 @@ def test_fused_int8_one_two_beams(context, command_queue, A, T, M, signed):
     np.testing.assert_array_equal(q, O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, batch_dt=bdt, scale=1 / 32,
                                                            signed=signed))
     assert np.abs(q.astype(int)).max() >= 4
+    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=signed,
+                                 batch_dt=bdt).instantiate(command_queue)
+    (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    assert_beams_allclose(y, O.fused_beamform(raw, d, Ctot, xeng_id=xeng, batch_dt=bdt, signed=signed),
+                          O.reorder(raw), O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, batch_dt=bdt), signed=signed)
 
 
 def test_fused_int8_float_path_is_requantised_f32(context, command_queue, monkeypatch):
