@@ -863,7 +863,8 @@ __device__ __forceinline__ void i8_store_block(const uint32_t (&pk)[NTS][4], int
 // fragments, 8 i8 MFMAs per (sample, tile), requantise, 4-byte stores.
 // Mode (diagnostics only): kSkipCoef / kSkipMfma / kSkipStore / kSkipLoad as the float item kernel; 16 = fast
 // (f32 sincos) coefficients only (inexact); 128 = exact coefficients only (no fast attempt).
-template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3>
+// A64: exactly 64 antennas and every in-item offset below 2^32 (the launcher checks), so no antenna is clamped.
+template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3, bool A64 = false>
 __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -889,6 +890,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
   if constexpr (!(Mode & kSkipCoef)) load_delays<NTS>(cp, P, c, tau0, nts, tid);
   __builtin_amdgcn_sched_barrier(0);
   const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+  const uint32_t loff64 = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride) + tqc * 16u;  // A64 only
   uint32_t d[2][8][4];
 #pragma unroll
   for (int ss = 0; ss < 2; ++ss) {
@@ -901,9 +903,14 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      int a = 32 * ss + 8 * h + q;
-      a = a < P.A ? a : P.A - 1;
-      const u32x4_t* src = reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a) * ant_stride + tqc * 16u);
+      const u32x4_t* src;
+      if constexpr (A64) {  // wave-uniform base + one 32-bit lane offset: no per-load VALU address arithmetic
+        src = reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(32 * ss + q) * ant_stride + loff64);
+      } else {
+        int a = 32 * ss + 8 * h + q;
+        a = a < P.A ? a : P.A - 1;
+        src = reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a) * ant_stride + tqc * 16u);
+      }
       const u32x4_t v = (Mode & kI8PlainLoad) ? *src : __builtin_nontemporal_load(src);
       d[ss][q][0] = v[0];
       d[ss][q][1] = v[1];
@@ -1075,8 +1082,14 @@ int launch_i8_item(FusedArgs P, hipStream_t st, size_t min_lds = 0) {
   const size_t lds = std::max<size_t>(static_cast<size_t>(2) * NTS * 2 * 64 * 16 + 4 * 32 * 4, min_lds);
   const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
   BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many items");
-  hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ>),
-                     dim3(static_cast<unsigned>(n_items)), dim3(kThreads), lds, st, P);
+  const char* ae = getenv("BF_I8_A64");  // measurement: 0 forces the clamped per-lane addressing
+  const bool a64 = P.A == 64 && 24ull * P.C * P.T * 4 + P.T * 4ull < (1ull << 32) && !(ae && ae[0] == '0');
+  if (a64)
+    hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ, true>),
+                       dim3(static_cast<unsigned>(n_items)), dim3(kThreads), lds, st, P);
+  else
+    hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ, false>),
+                       dim3(static_cast<unsigned>(n_items)), dim3(kThreads), lds, st, P);
   BF_LAUNCHED("beamform_fused_i8_item_kernel");
 }
 

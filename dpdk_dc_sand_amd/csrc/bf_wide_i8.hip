@@ -143,30 +143,31 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(F
     const int cd = P.delay_channels == 1 ? 0 : c;
     const int npairs = 32 * Sp * kW8Beams;
     int cs0 = 0, cs1 = 0;
+    // pair e = tid + 256 J of this thread: beam row ml = (tid >> 2) % 16 (the same for every J) and slot antenna
+    // sa0 + 16 J -- the per-pair index arithmetic reduces to one add
+    const int ml = (tid >> 2) & (kW8Beams - 1);
+    const int sa0 = 4 * (tid >> 6) + (tid & 3);
+    const int m = m0 + ml;
+    const bool m_ok = m < P.M;
+    const float4* dv_row = P.dv + (static_cast<size_t>(cd) * P.M + min(m, P.M - 1)) * P.A;
+    const float* g_row = P.gain ? P.gain + static_cast<size_t>(min(m, P.M - 1)) * P.A : nullptr;
+    const int nj = npairs / kW8Threads;  // 2 Sp
+    const int off0 = coef8_byte(2 * sa0, 2 * ml, 2, 0);
     constexpr int kBatch = 8;
-    for (int e0 = tid; e0 < npairs; e0 += kBatch * kW8Threads) {
+    for (int j0 = 0; j0 < nj; j0 += kBatch) {
       float4 dv[kBatch];
       float gv[kBatch];
-#pragma unroll
-      for (int j = 0; j < kBatch; ++j) {
-        if constexpr (Mode & 1) break;
-        const int e = e0 + j * kW8Threads;
-        const int sa = 4 * ((e >> 2) / kW8Beams) + (e & 3);
-        const int a = min(w8_step_base(sa >> 5, P.A) + (sa & 31), P.A - 1);
-        const int m = min(m0 + (e >> 2) % kW8Beams, P.M - 1);
-        dv[j] = P.dv[(static_cast<size_t>(cd) * P.M + m) * P.A + a];
-        gv[j] = 1.0f;
-        if (P.gain) gv[j] = P.gain[m * P.A + a];
-      }
       bool valid[kBatch];
       int wc[kBatch], ws[kBatch];
 #pragma unroll
       for (int j = 0; j < kBatch; ++j) {
-        const int e = e0 + j * kW8Threads;
-        const int sa = 4 * ((e >> 2) / kW8Beams) + (e & 3);
-        const int a = w8_step_base(sa >> 5, P.A) + (sa & 31);
+        const int sa = sa0 + 16 * (j0 + j), st = sa >> 5;
+        const int a = w8_step_base(st, P.A) + (sa & 31);
         // rows of antennas an earlier step already covered stay zero
-        valid[j] = e < npairs && a >= 32 * (sa >> 5) && m0 + (e >> 2) % kW8Beams < P.M;
+        valid[j] = j0 + j < nj && m_ok && a >= 32 * st;
+        if constexpr (Mode & 1) continue;
+        dv[j] = dv_row[min(a, P.A - 1)];
+        gv[j] = g_row ? g_row[min(a, P.A - 1)] : 1.0f;
       }
       if constexpr (Mode & 1) {
 #pragma unroll
@@ -179,29 +180,18 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(F
       }
 #pragma unroll
       for (int j = 0; j < kBatch; ++j) {
-        const int e = e0 + j * kW8Threads;
-        if (e >= npairs) break;
-        const int ml = (e >> 2) % kW8Beams;
-        const int sa = 4 * ((e >> 2) / kW8Beams) + (e & 3);
-        const int Wc = wc[j], Ws = ws[j];
-        const int cl = 2 * ml;
-        // (k, k + 1) = (2 sa, 2 sa + 1) are adjacent bytes of one column: one 16-bit write per (column, limb)
-        const int col_w[2][2] = {{Wc, -Ws}, {Ws, Wc}};  // [column cl + e][k = 2 sa + f]
-#pragma unroll
-        for (int ec = 0; ec < 2; ++ec) {
-          int h2[2], l2[2];
-#pragma unroll
-          for (int f = 0; f < 2; ++f) {
-            const int W = col_w[ec][f];
-            l2[f] = ((W + 128) & 255) - 128;
-            h2[f] = (W - l2[f]) >> 8;
-          }
-          const int off = coef8_byte(2 * sa, cl + ec, 2, 0);
-          *reinterpret_cast<uint16_t*>(lb + off) =
-              static_cast<uint16_t>((h2[0] & 255) | ((h2[1] & 255) << 8));
-          *reinterpret_cast<uint16_t*>(lb + off + 64 * 16) =
-              static_cast<uint16_t>((l2[0] & 255) | ((l2[1] & 255) << 8));
-        }
+        if (j0 + j >= nj) break;
+        const int J = j0 + j;
+        const int Wc = wc[j], Ws = ws[j], nWs = -Ws;
+        // Column 2 ml holds (k = 2 sa, 2 sa + 1) = (Wc, -Ws), column 2 ml + 1 holds (Ws, Wc): one 16-bit write per
+        // (column, limb).  Balanced limbs W = 256 hi + lo, lo in [-128, 127]: lo's byte is W's byte 0 and hi's byte
+        // is byte 1 of W + 128, so each pair of limb bytes is one v_perm.  Pair J's image offset is the thread's
+        // base plus a constant (k = 2 sa0 + 32 J with 2 sa0 < 32: step J >> 1, lane group + 2 (J & 1)).
+        int8_t* o = lb + off0 + 4096 * (J >> 1) + 512 * (J & 1);
+        *reinterpret_cast<uint16_t*>(o) = static_cast<uint16_t>(__builtin_amdgcn_perm(nWs + 128, Wc + 128, 0x0c0c0501u));
+        *reinterpret_cast<uint16_t*>(o + 64 * 16) = static_cast<uint16_t>(__builtin_amdgcn_perm(nWs, Wc, 0x0c0c0400u));
+        *reinterpret_cast<uint16_t*>(o + 16) = static_cast<uint16_t>(__builtin_amdgcn_perm(Wc + 128, Ws + 128, 0x0c0c0501u));
+        *reinterpret_cast<uint16_t*>(o + 16 + 64 * 16) = static_cast<uint16_t>(__builtin_amdgcn_perm(Wc, Ws, 0x0c0c0400u));
         cs0 += Wc - Ws;  // column 2m:   W[2a][2m] + W[2a+1][2m]
         cs1 += Ws + Wc;  // column 2m+1: W[2a][2m+1] + W[2a+1][2m+1]
       }

@@ -100,6 +100,16 @@ names_i8 = {0: "full (fast+fixup coef, occ 3)", 128: "exact-only coef", 16: "fas
             4096: "occ4 (spills)", 7168: "occ4 serial+pol", 6144: "occ4 pol order",
             8192: "plain stores", 16384: "plain loads", 24576: "plain loads+stores"}
 alg_i8 = nin + nout // 4
+if _os.environ.get("I8_AB"):  # interleaved A/B: int8 item kernel with uniform-base (A == 64) vs clamped addressing
+    ab = {"uniform": [], "clamped": []}
+    for r in range(ROUNDS):
+        for form, val in (("uniform", "1"), ("clamped", "0")):
+            _os.environ["BF_I8_A64"] = val
+            ab[form].append(timeit(lambda i: lib.bf_diag_fused(512, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
+                                                               B, C, T, A, M, C, 1 / 1712e6, q.handle)))
+    for form, ts in ab.items():
+        ts = sorted(ts)
+        print(f"  i8 full, {form:8s} addressing  median {ts[len(ts) // 2] * 1e6:8.1f} us  min {ts[0] * 1e6:8.1f} us")
 for kbase, kname in ((0, "pipe"), (32, "item"), (512, "i8")):
     if _os.environ.get("DIAG_KERNELS", "item,pipe,i8").find(kname) < 0:
         continue
