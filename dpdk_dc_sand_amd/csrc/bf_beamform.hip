@@ -164,28 +164,30 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
   const int K2 = 2 * A, M2 = 2 * M;
   const int Sp = (S + R - 1) / R * R;  // padded steps per row group
 
-  stage_table<NTS>(reinterpret_cast<_Float16*>(lds), w + bpc * static_cast<size_t>(K2) * M2, K2, M2, Sp, tau0, nts,
-                   tid);  // padded steps zero
-  __syncthreads();
-
   const int T = NB * kSamplesPerBlock;
   const uint8_t* xp = x + bpc * static_cast<size_t>(T) * K2;
   float* yp = y + bpc * static_cast<size_t>(T) * M2;
   const int h = lane >> 4, tl = lane & 15;
   const int nrg = (NB - wave + kWaves - 1) / kWaves;  // this wave's row groups (rg = wave + 4 j)
-  if (nrg <= 0) return;
-  const int nsteps = nrg * Sp;  // the wave's whole fragment stream
+  const int nsteps = max(nrg, 1) * Sp;  // the wave's whole fragment stream (a wave without rows streams row 0)
   // stream position q -> (row group j = q / Sp, step s = q % Sp); byte offset of the lane's 8 bytes, clamped
   auto src = [&](int q) -> const uint2* {
     q = min(q, nsteps - 1);
     const int j = q / Sp, s = q - j * Sp;
-    const int tt = (wave + kWaves * j) * kSamplesPerBlock + tl;
+    const int tt = min((wave + kWaves * j) * kSamplesPerBlock + tl, T - 1);  // in the item even for row-less waves
     const int k0 = min(32 * s + 8 * h, K2 - 8);
     return reinterpret_cast<const uint2*>(xp + static_cast<size_t>(tt) * K2 + k0);
   };
+  // the ring's first R fragments are requested BEFORE the coefficient table: vmcnt counts in order, so the table
+  // conversion's wait then covers both, and the voltage latency overlaps the table's
   uint2 ring[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) ring[r] = *src(r);
+  __builtin_amdgcn_sched_barrier(0);
+  stage_table<NTS>(reinterpret_cast<_Float16*>(lds), w + bpc * static_cast<size_t>(K2) * M2, K2, M2, Sp, tau0, nts,
+                   tid);  // padded steps zero
+  __syncthreads();
+  if (nrg <= 0) return;
 
   f32x4 acc[NTS];
 #pragma unroll
@@ -256,7 +258,10 @@ int dispatch_vec(const uint8_t* x, const float* w, float* y, long long bpc, int 
       return launch_ring<Signed, NTS, 16>(x, w, y, bpc, NB, A, M, S, NT, st);
     if (S >= 8 && coef_lds_bytes((S + 7) / 8 * 8, NTS) <= kMaxLds)
       return launch_ring<Signed, NTS, 8>(x, w, y, bpc, NB, A, M, S, NT, st);
-    // (below 8 k-steps the basic kernel's small LDS footprint keeps enough workgroups resident to hide latency)
+    // 4..7 k-steps (64 antennas: config 3): a 4-deep ring
+    const char* r4 = getenv("BF_TABLE_RING4");  // measurement: 0 keeps the basic kernel
+    if (S >= 4 && !(r4 && r4[0] == '0') && coef_lds_bytes((S + 3) / 4 * 4, NTS) <= kMaxLds)
+      return launch_ring<Signed, NTS, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
   }
   if (A % 4 == 0) return launch_table<Signed, NTS, true>(x, w, y, bpc, NB, A, M, S, NT, st);
   return launch_table<Signed, NTS, false>(x, w, y, bpc, NB, A, M, S, NT, st);

@@ -180,7 +180,8 @@ def test_beamform(context, command_queue, n_batches, n_ants, n_channels, n_sampl
 
 @pytest.mark.parametrize("A,M,C,T,signed", [
     (64, 16, 4, 256, False), (64, 16, 4, 256, True), (19, 3, 5, 64, False), (5, 1, 3, 32, True),
-    (130, 9, 2, 48, False), (256, 64, 1, 32, False), (61, 8, 3, 16, True), (2, 40, 2, 16, False)])
+    (130, 9, 2, 48, False), (256, 64, 1, 32, False), (61, 8, 3, 16, True), (2, 40, 2, 16, False),
+    (64, 4, 2, 16, True), (96, 16, 2, 48, False)])
 def test_matrix_multiply_random_tables(context, command_queue, A, M, C, T, signed):
     """Per-beam-varying coefficients (which the reference CPU oracle gets wrong) and int8 samples."""
     B = 2
