@@ -1324,12 +1324,37 @@ __global__ __launch_bounds__(256) void stream_kernel(const uint4* __restrict__ i
     }
   }
 }
+// The int8 path's traffic mix as a stream: 4 bytes read per byte written, uniformly over time (out[i] = xor of
+// four in-streams), non-temporal loads (and stores when NtStore).
+template <bool NtStore>
+__global__ __launch_bounds__(256) void stream_mix_kernel(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                         size_t n_out) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_out; i += stride) {
+    u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + i));
+#pragma unroll
+    for (int u = 1; u < 4; ++u) a ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + i + u * n_out));
+    if constexpr (NtStore)
+      __builtin_nontemporal_store(a, reinterpret_cast<u32x4*>(out + i));
+    else
+      *reinterpret_cast<u32x4*>(out + i) = a;
+  }
+}
 }  // namespace bf
 
 extern "C" int bf_diag_stream(const void* in, void* out, size_t in_bytes, size_t out_bytes, int grid, int unroll,
                               void* stream) {
   auto in4 = reinterpret_cast<const uint4*>(in);
   auto out4 = reinterpret_cast<uint4*>(out);
+  if (unroll == 200 || unroll == 201) {  // the 4:1 read:write mix (out_bytes = in_bytes / 4)
+    if (unroll == 200)
+      hipLaunchKernelGGL((bf::stream_mix_kernel<true>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
+                         out_bytes / 16);
+    else
+      hipLaunchKernelGGL((bf::stream_mix_kernel<false>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
+                         out_bytes / 16);
+    BF_LAUNCHED("stream_mix_kernel");
+  }
   if (unroll == 101)
     hipLaunchKernelGGL((bf::stream_kernel<1, false, true>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
                        in_bytes / 16, out_bytes / 16);

@@ -129,6 +129,12 @@ for kbase, kname in ((0, "pipe"), (32, "item"), (512, "i8")):
         nm, ab = (names_i8[mode], alg_i8) if kname == "i8" else (names[mode], alg)
         print(f"  {kname} mode {mode:3d} {nm:18s} median {med*1e6:8.1f} us  min {mn*1e6:8.1f} us  "
               f"alg {ab/med/1e9:7.1f} GB/s  ({len(ts)} rounds)")
+if _os.environ.get("DIAG_MIX"):  # the int8 path's 4:1 read:write mix, uniformly interleaved
+    for grid in (1024, 2048, 4096, 8192, 16384):
+        for code, nm in ((200, "nt load+store"), (201, "nt load")):
+            t = timeit(lambda i: lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, nin, nin // 4, grid, code,
+                                                    q.handle))
+            print(f"  mix grid {grid:5d} {nm:14s} {t*1e6:8.1f} us  {(nin + nin // 4)/t/1e9:7.1f} GB/s")
 if _os.environ.get("DIAG_STREAMS", "1") == "1":
     for grid in (512, 1024, 2048):
         for unroll, uname in ((1, "plain"), (101, "nt-store"), (102, "nt-load"), (103, "nt-both")):
