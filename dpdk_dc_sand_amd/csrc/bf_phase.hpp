@@ -109,7 +109,9 @@ __device__ __forceinline__ double steering_coeff_fast(float4 dv, double chc, dou
   const float pc = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f),
                              z * z, -0.5f * z), 1.0f, 1.0f);
   const float s1 = fmaf(pc, dr, ps), c1 = fmaf(-ps, dr, pc);  // sin, cos of r = rf + dr
-  const int q = static_cast<int>(static_cast<long long>(n) & 3);
+  // quadrant by one saturating v_cvt_i32_f64 (the 64-bit conversion costs four float64 instructions); exact for
+  // |n| < 2^31, i.e. |rot| < 3.4e9 rad, far beyond where a float64 rotation still carries phase information
+  const int q = __double2int_rn(n) & 3;
   const float s0 = (q & 1) ? c1 : s1, c0 = (q & 1) ? s1 : c1;
   *re = ((q + 1) & 2) ? -c0 : c0;
   *im = (q & 2) ? -s0 : s0;

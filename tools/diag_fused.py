@@ -57,7 +57,7 @@ print(f"shape B={B} C={C} T={T} A={A} M={M}: in {nin/2**30:.2f} GiB out {nout/2*
 ROUNDS = int(_os.environ.get("DIAG_ROUNDS", "1"))
 if "wide" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_wide.argtypes = [I, I, V, V, V, I, I, I, I, I, I, D, V]
-    wnames = {64: "occ 4 bound", 96: "occ 3 bound", 0: "full (fast coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 3: "no-coef,no-mfma",
+    wnames = {0: "full (fast coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 3: "no-coef,no-mfma",
               5: "no-coef,no-store"}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
     for tw in (2, 1):
