@@ -39,6 +39,8 @@ constexpr int kCachedLoad = 128, kNtStore = 256;
 constexpr int kSerialCoef = 1024, kPolOrder = 2048;
 // Cache-policy variants of the integer item kernel (which streams with non-temporal loads and stores).
 constexpr int kI8PlainStore = 8192, kI8PlainLoad = 16384;
+// Wave-priority variants (s_setprio 3): while issuing the item's loads / during the store phase.
+constexpr int kPrioLoads = 1 << 16, kPrioStores = 1 << 17;
 
 // One group of 4 k-steps: 16 x 16-byte loads per lane, all UNCONDITIONAL: out-of-range antennas (a >= A) read
 // antenna A-1 and meet zero coefficient rows, out-of-range time quads read the last quad and are never stored,
@@ -886,6 +888,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
   int* colsum = reinterpret_cast<int*>(lb + static_cast<size_t>(2) * NTS * 2 * 64 * 16);
 
   // 1. delay model (oldest), 2. voltages, 3. coefficients under them
+  if constexpr ((Mode & kPrioLoads) != 0) __builtin_amdgcn_s_setprio(3);
   CoefPrefetch<NTS> cp;
   if constexpr (!(Mode & kSkipCoef)) load_delays<NTS>(cp, P, c, tau0, nts, tid);
   __builtin_amdgcn_sched_barrier(0);
@@ -919,6 +922,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
     }
   }
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr ((Mode & kPrioLoads) != 0) __builtin_amdgcn_s_setprio(0);
   i8_coef_phase<Signed, NTS, Mode>(lb, colsum, cp, P, b, c, tau0, nts, S8, tid, lane, wave);
   __syncthreads();
   const int4* fr = reinterpret_cast<const int4*>(lds);
@@ -929,6 +933,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
   constexpr bool kTile = Full && !(Mode & (kSkipMfma | kSkipStore | kSkipLoad | kPolOrder));
   uint32_t pkall[2][NTS][4];
   if constexpr (kTile) i8_contract_rows<Signed, NTS>(fr, d, colsum, s32, S8, lane, h, pkall);
+  if constexpr ((Mode & kPrioStores) != 0) __builtin_amdgcn_s_setprio(3);
 
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -1421,6 +1426,8 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 4096: return bf::launch_i8_item<true, 2, true, 0, 4>(P, st);
       case 4096 + 3072: return bf::launch_i8_item<true, 2, true, 3072, 4>(P, st);
       case 4096 + 2048: return bf::launch_i8_item<true, 2, true, 2048, 4>(P, st);
+      case 65536: return bf::launch_i8_item<true, 2, true, 65536>(P, st);
+      case 131072: return bf::launch_i8_item<true, 2, true, 131072>(P, st);
       case 8192: return bf::launch_i8_item<true, 2, true, 8192>(P, st);
       case 16384: return bf::launch_i8_item<true, 2, true, 16384>(P, st);
       case 8192 + 16384: return bf::launch_i8_item<true, 2, true, 8192 + 16384>(P, st);
