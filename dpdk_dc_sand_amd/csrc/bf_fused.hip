@@ -31,7 +31,7 @@ constexpr int kSkipCoef = 1, kSkipMfma = 2, kSkipStore = 4, kSkipLoad = 8;
 // Cache-policy bits for measurement: the product streams voltages with non-temporal loads (read once: -1.8 %
 // time, profiles/r1_v2_ablation_nt.txt); kCachedLoad selects plain loads, kNtStore non-temporal beam stores
 // (slower: +17 %).
-constexpr int kCachedLoad = 128, kNtStore = 256;
+constexpr int kCachedLoad = 128, kNtStore = 256, kMapChannelFastF32 = 512;
 // Integer item kernel layout variants (A/B-measured in the diagnostic build, profiles/r1_v7_i8_variants.txt):
 // kSerialCoef evaluates the fast Q14 phasors one at a time (fewer live float64 temporaries: no gain), kPolOrder
 // restores the pol-outermost contraction of full slabs (the product runs sample-row-outermost with immediate
@@ -41,6 +41,24 @@ constexpr int kSerialCoef = 1024, kPolOrder = 2048;
 constexpr int kI8PlainStore = 8192, kI8PlainLoad = 16384;
 // Wave-priority variants (s_setprio 3): while issuing the item's loads / during the store phase.
 constexpr int kPrioLoads = 1 << 16, kPrioStores = 1 << 17;
+// Workgroup order variant: consecutive workgroups take consecutive batches of a channel instead of channels.
+constexpr int kMapBatchFast = 1 << 18, kMapXcdBatch = 1 << 19, kMapXcdRange = 1 << 20, kMapChannelFast = 1 << 21;
+
+// Workgroup -> (batch, channel) of an item kernel.  Workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8),
+// so with channel-fastest numbering every XCD reads every 8th KiB run of each antenna stream.  XCD-range order
+// gives XCD x the contiguous channel range [x C/8, (x+1) C/8), channel fastest within it and batches outermost:
+// each XCD's resident workgroups stream one contiguous window per antenna (cfg3 int8: 461 -> 434 us,
+// profiles/r1_v8_i8_order.txt).  Needs C % 8 == 0 (otherwise channel-fastest).  The slab index stays outermost.
+__device__ __forceinline__ void item_coords(int item, int C, int B, bool xcd_range, int* b, int* c) {
+  if (xcd_range) {
+    const int xcd = item & 7, local = (item >> 3) % (B * (C >> 3));
+    *b = local / (C >> 3);
+    *c = xcd * (C >> 3) + local % (C >> 3);
+  } else {
+    *c = item % C;
+    *b = (item / C) % B;
+  }
+}
 
 // One group of 4 k-steps: 16 x 16-byte loads per lane, all UNCONDITIONAL: out-of-range antennas (a >= A) read
 // antenna A-1 and meet zero coefficient rows, out-of-range time quads read the last quad and are never stored,
@@ -393,8 +411,13 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_item_kernel(Fuse
   const bool tv = tq < T4;
   const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
   const int item = blockIdx.x;
-  const int c = item % P.C;
-  const int b = (item / P.C) % P.B;
+  int b, c;
+  if constexpr ((Mode & kMapChannelFastF32) != 0) {  // diagnostics: the earlier channel-fastest order
+    c = item % P.C;
+    b = (item / P.C) % P.B;
+  } else {
+    item_coords(item, P.C, P.B, P.xcd_order != 0, &b, &c);
+  }
   const int slab = item / (P.C * P.B);
   const int tau0 = slab * NTS;
   const int nts = Full ? NTS : min(NTS, P.NT - tau0);
@@ -877,8 +900,27 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
   const int tqc = tv ? tq : T4 - 1;
   const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
   const int item = blockIdx.x;
-  const int c = item % P.C;
-  const int b = (item / P.C) % P.B;
+  // item -> (b, c): XCD-range order (item_coords); diagnostics: kMapChannelFast (channel fastest, the earlier
+  // order), kMapBatchFast (batch fastest), kMapXcdBatch (XCD x: channels == x mod 8, batch fastest), kMapXcdRange
+  // (XCD-range, batch fastest)
+  int c, b;
+  if constexpr ((Mode & kMapXcdRange) != 0) {
+    const int xcd = item & 7, local = (item >> 3) % (P.B * (P.C >> 3));
+    b = local % P.B;
+    c = xcd * (P.C >> 3) + local / P.B;
+  } else if constexpr ((Mode & kMapXcdBatch) != 0) {
+    const int xcd = item & 7, local = (item >> 3) % (P.B * (P.C >> 3));
+    b = local % P.B;
+    c = (local / P.B) * 8 + xcd;
+  } else if constexpr ((Mode & kMapBatchFast) != 0) {
+    c = (item / P.B) % P.C;
+    b = item % P.B;
+  } else if constexpr ((Mode & kMapChannelFast) != 0) {
+    c = item % P.C;
+    b = (item / P.C) % P.B;
+  } else {
+    item_coords(item, P.C, P.B, P.xcd_order != 0, &b, &c);
+  }
   const int slab = item / (P.C * P.B);
   const int tau0 = slab * NTS;
   const int nts = Full ? NTS : min(NTS, P.NT - tau0);
@@ -1081,9 +1123,18 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
   }
 }
 
+// Workgroup order of the item kernels (item_coords): XCD-range when C % 8 == 0, unless BF_ITEM_ORDER=channel.
+bool item_xcd_order(const FusedArgs& P) {
+  const char* e = getenv("BF_ITEM_ORDER");
+  if (e && e[0] == 'c') return false;
+  if (e && e[0] == 'x') return (P.C & 7) == 0;
+  return (P.C & 7) == 0;
+}
+
 template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3>
 int launch_i8_item(FusedArgs P, hipStream_t st, size_t min_lds = 0) {
   P.nslabs = (P.NT + NTS - 1) / NTS;
+  P.xcd_order = item_xcd_order(P);
   const size_t lds = std::max<size_t>(static_cast<size_t>(2) * NTS * 2 * 64 * 16 + 4 * 32 * 4, min_lds);
   const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
   BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many items");
@@ -1167,6 +1218,7 @@ int launch_pipe(FusedArgs P, hipStream_t st) {
 template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0, int Occ = 1>
 int launch_item(FusedArgs P, hipStream_t st) {
   P.nslabs = (P.NT + NTS - 1) / NTS;
+  P.xcd_order = item_xcd_order(P);
   const size_t lds = coef_lds_bytes(P.S, NTS);
   const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
   BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many (batch, channel) items");
@@ -1426,6 +1478,10 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 4096: return bf::launch_i8_item<true, 2, true, 0, 4>(P, st);
       case 4096 + 3072: return bf::launch_i8_item<true, 2, true, 3072, 4>(P, st);
       case 4096 + 2048: return bf::launch_i8_item<true, 2, true, 2048, 4>(P, st);
+      case 262144: return bf::launch_i8_item<true, 2, true, 262144>(P, st);
+      case 524288: return bf::launch_i8_item<true, 2, true, 524288>(P, st);
+      case 1048576: return bf::launch_i8_item<true, 2, true, 1048576>(P, st);
+      case 2097152: return bf::launch_i8_item<true, 2, true, 2097152>(P, st);  // channel fastest (earlier order)
       case 65536: return bf::launch_i8_item<true, 2, true, 65536>(P, st);
       case 131072: return bf::launch_i8_item<true, 2, true, 131072>(P, st);
       case 8192: return bf::launch_i8_item<true, 2, true, 8192>(P, st);
@@ -1452,6 +1508,7 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 384: return bf::launch_item<true, false, 2, false, true, 384>(P, st);
       case 64: return bf::launch_item<true, false, 2, false, true, 0, 4>(P, st);  // 4 waves per SIMD bound
       case 96: return bf::launch_item<true, false, 2, false, true, 0, 3>(P, st);  // 3 waves per SIMD bound
+      case 160: return bf::launch_item<true, false, 2, false, true, 512>(P, st);  // channel-fastest order
       default: bf::set_error("bad mode"); return BF_ERR_ARG;
     }
   }

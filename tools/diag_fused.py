@@ -50,7 +50,7 @@ def timeit(fn, n=20):
     return e1.time_since(e0) / n
 
 
-names = {64: "occ 4 bound", 96: "occ 3 bound", 0: "full (fast coef)", 128: "cached loads", 256: "nt stores", 384: "cached loads+nt st",
+names = {64: "occ 4 bound", 96: "occ 3 bound", 160: "channel-fastest (old)", 0: "full (fast coef)", 128: "cached loads", 256: "nt stores", 384: "cached loads+nt st",
          16: "full (exact coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
          3: "no-coef,no-mfma", 5: "no-coef,no-store", 9: "no-coef,no-load", 7: "loads only", 11: "stores only"}
 print(f"shape B={B} C={C} T={T} A={A} M={M}: in {nin/2**30:.2f} GiB out {nout/2**30:.2f} GiB")
@@ -98,7 +98,7 @@ names_i8 = {0: "full (fast+fixup coef, occ 3)", 128: "exact-only coef", 16: "fas
             5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
             65: "occ 2, no-store", 1024: "serial coef", 2048: "pol order", 3072: "serial+pol order",
             4096: "occ4 (spills)", 7168: "occ4 serial+pol", 6144: "occ4 pol order",
-            65536: "prio while loading", 131072: "prio while storing", 8192: "plain stores", 16384: "plain loads", 24576: "plain loads+stores"}
+            262144: "batch-fastest order", 524288: "xcd x batch order", 1048576: "xcd range, batch fast", 2097152: "channel-fastest (old)", 65536: "prio while loading", 131072: "prio while storing", 8192: "plain stores", 16384: "plain loads", 24576: "plain loads+stores"}
 alg_i8 = nin + nout // 4
 if _os.environ.get("I8_AB"):  # interleaved A/B: int8 item kernel with uniform-base (A == 64) vs clamped addressing
     ab = {"uniform": [], "clamped": []}
