@@ -1123,12 +1123,14 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
   }
 }
 
-// Workgroup order of the item kernels (item_coords): XCD-range when C % 8 == 0, unless BF_ITEM_ORDER=channel.
+// Workgroup order of the item kernels (item_coords): XCD-range when C % 8 == 0 and the beams are at least 8 (config
+// 3: 450-461 -> 432-433 us); channel-fastest for one or two beams, whose read-dominated traffic measured no better
+// that way (config 2: 334-357 vs 332-340 us, profiles/r1_v8_order_bench_ab.txt).  BF_ITEM_ORDER=xcd|channel forces.
 bool item_xcd_order(const FusedArgs& P) {
   const char* e = getenv("BF_ITEM_ORDER");
   if (e && e[0] == 'c') return false;
   if (e && e[0] == 'x') return (P.C & 7) == 0;
-  return (P.C & 7) == 0;
+  return (P.C & 7) == 0 && P.M >= 8;
 }
 
 template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3>
