@@ -31,7 +31,8 @@ constexpr int kSkipCoef = 1, kSkipMfma = 2, kSkipStore = 4, kSkipLoad = 8;
 // Cache-policy bits for measurement: the product streams voltages with non-temporal loads (read once: -1.8 %
 // time, profiles/r1_v2_ablation_nt.txt); kCachedLoad selects plain loads, kNtStore non-temporal beam stores
 // (slower: +17 %).
-constexpr int kCachedLoad = 128, kNtStore = 256, kMapChannelFastF32 = 512;
+constexpr int kCachedLoad = 128, kNtStore = 256, kMapChannelFastF32 = 512, kMapBatchFastF32 = 1024,
+              kMapXcdBatchF32 = 2048;
 // Integer item kernel layout variants (A/B-measured in the diagnostic build, profiles/r1_v7_i8_variants.txt):
 // kSerialCoef evaluates the fast Q14 phasors one at a time (fewer live float64 temporaries: no gain), kPolOrder
 // restores the pol-outermost contraction of full slabs (the product runs sample-row-outermost with immediate
@@ -415,6 +416,13 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_item_kernel(Fuse
   if constexpr ((Mode & kMapChannelFastF32) != 0) {  // diagnostics: the earlier channel-fastest order
     c = item % P.C;
     b = (item / P.C) % P.B;
+  } else if constexpr ((Mode & kMapBatchFastF32) != 0) {  // diagnostics: batch fastest
+    c = (item / P.B) % P.C;
+    b = item % P.B;
+  } else if constexpr ((Mode & kMapXcdBatchF32) != 0) {  // diagnostics: XCD x -> channels == x mod 8, batch fastest
+    const int xcd = item & 7, local = (item >> 3) % (P.B * (P.C >> 3));
+    b = local % P.B;
+    c = (local / P.B) * 8 + xcd;
   } else {
     item_coords(item, P.C, P.B, P.xcd_order != 0, &b, &c);
   }
@@ -1511,6 +1519,9 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 64: return bf::launch_item<true, false, 2, false, true, 0, 4>(P, st);  // 4 waves per SIMD bound
       case 96: return bf::launch_item<true, false, 2, false, true, 0, 3>(P, st);  // 3 waves per SIMD bound
       case 160: return bf::launch_item<true, false, 2, false, true, 512>(P, st);  // channel-fastest order
+      case 192: return bf::launch_item<true, false, 2, false, true, 1024>(P, st);  // batch-fastest order
+      case 224: return bf::launch_item<true, false, 2, false, true, 2048>(P, st);  // XCD x batch order
+      case 288: return bf::launch_item<true, false, 2, false, true, 256>(P, st);  // nt stores
       default: bf::set_error("bad mode"); return BF_ERR_ARG;
     }
   }

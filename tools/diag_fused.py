@@ -50,7 +50,8 @@ def timeit(fn, n=20):
     return e1.time_since(e0) / n
 
 
-names = {64: "occ 4 bound", 96: "occ 3 bound", 160: "channel-fastest (old)", 0: "full (fast coef)", 128: "cached loads", 256: "nt stores", 384: "cached loads+nt st",
+names = {64: "occ 4 bound", 96: "occ 3 bound", 160: "channel-fastest (old)", 192: "batch-fastest", 224: "xcd x batch",
+         288: "nt stores (xcd)", 0: "full (fast coef)", 128: "cached loads", 256: "nt stores", 384: "cached loads+nt st",
          16: "full (exact coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
          3: "no-coef,no-mfma", 5: "no-coef,no-store", 9: "no-coef,no-load", 7: "loads only", 11: "stores only"}
 print(f"shape B={B} C={C} T={T} A={A} M={M}: in {nin/2**30:.2f} GiB out {nout/2**30:.2f} GiB")
