@@ -342,6 +342,28 @@ def test_fused_int8_one_two_beams(context, command_queue, A, T, M, signed):
                           O.reorder(raw), O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, batch_dt=bdt), signed=signed)
 
 
+@pytest.mark.parametrize("order", ["xcd", "channel"])
+@pytest.mark.parametrize("B,C,M", [(2, 16, 16), (3, 24, 8), (1, 8, 16), (2, 40, 12)])
+def test_item_kernels_workgroup_order(context, command_queue, monkeypatch, order, B, C, M):
+    """The item kernels' XCD-range workgroup order (C % 8 == 0, >= 8 beams; item_coords) covers every (batch,
+    channel) exactly once: int8 bit-exact and f32 within the tolerance, in both orders."""
+    monkeypatch.setenv("BF_ITEM_ORDER", order)
+    A, T, Ctot, xeng, bdt = 64, 256, 8 * C, 1, 256 * 8192 * TS
+    d = random_delays(1, M, A, B * C + M)
+    rng = np.random.default_rng(C * 3 + M)
+    raw = rng.integers(-128, 128, (B, A, C, T, 2, 2), dtype=np.int8)
+    q8 = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=True,
+                                 out_int8=True, out_scale=1 / 64, batch_dt=bdt).instantiate(command_queue)
+    (q,) = run(q8, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    np.testing.assert_array_equal(q, O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, batch_dt=bdt, scale=1 / 64,
+                                                           signed=True))
+    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=True,
+                                 batch_dt=bdt).instantiate(command_queue)
+    (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    assert_beams_allclose(y, O.fused_beamform(raw, d, Ctot, xeng_id=xeng, batch_dt=bdt, signed=True), O.reorder(raw),
+                          O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, batch_dt=bdt), signed=True)
+
+
 def test_fused_int8_float_path_is_requantised_f32(context, command_queue, monkeypatch):
     """Measurement path (BF_FUSED_INT8_FLOAT=1): float beams requantised in-kernel == bf_requant(float beams)."""
     monkeypatch.setenv("BF_FUSED_INT8_FLOAT", "1")
