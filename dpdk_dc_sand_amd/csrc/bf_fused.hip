@@ -892,11 +892,14 @@ __device__ __forceinline__ void i8_store_block(const uint32_t (&pk)[NTS][4], int
   }
 }
 
-// Item form of the integer kernel (A <= 64, T <= 256): one (slab, b, c) per workgroup, issue order delay model ->
-// voltages (16 x 16 B per lane) -> exact coefficients + Q14 limbs under them -> barrier -> per pol: v_perm
-// fragments, 8 i8 MFMAs per (sample, tile), requantise, 4-byte stores.
+// Item form of the integer kernel (A <= 64, T <= 256): one (slab, b, c) per workgroup in XCD-range order
+// (item_coords), issue order delay model -> voltages (16 x 16 B per lane, non-temporal) -> exact-contract
+// coefficients + Q14 limbs under them -> barrier -> full slabs: sample row outermost, both pols, 4 i8 MFMAs per
+// (row, pol, tile) requantised at once, row transpose + ds_bpermute into 1 KiB store blocks; partial slabs and
+// one/two beams: the per-pol path below.  3 waves per SIMD (launch bound; 4 spills).
 // Mode (diagnostics only): kSkipCoef / kSkipMfma / kSkipStore / kSkipLoad as the float item kernel; 16 = fast
-// (f32 sincos) coefficients only (inexact); 128 = exact coefficients only (no fast attempt).
+// (f32 sincos) coefficients only (inexact); 128 = exact coefficients only (no fast attempt); the layout, cache
+// policy, priority and workgroup-order variants defined above.
 // A64: exactly 64 antennas and every in-item offset below 2^32 (the launcher checks), so no antenna is clamped.
 template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3, bool A64 = false>
 __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(FusedArgs P) {
