@@ -44,7 +44,7 @@ constexpr int kI8PlainStore = 8192, kI8PlainLoad = 16384;
 constexpr int kPrioLoads = 1 << 16, kPrioStores = 1 << 17;
 // Workgroup order variant: consecutive workgroups take consecutive batches of a channel instead of channels.
 constexpr int kMapBatchFast = 1 << 18, kMapXcdBatch = 1 << 19, kMapXcdRange = 1 << 20, kMapChannelFast = 1 << 21,
-              kMapXcdFlat = 1 << 22;
+              kMapXcdFlat = 1 << 22, kMapXcdBlock = 1 << 23;
 
 // Workgroup -> (batch, channel) of an item kernel.  Workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8),
 // so with channel-fastest numbering every XCD reads every 8th KiB run of each antenna stream.  XCD-range order
@@ -920,6 +920,11 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
     const int xcd = item & 7, local = (item >> 3) % (P.B * (P.C >> 3));
     b = local % P.B;
     c = xcd * (P.C >> 3) + local / P.B;
+  } else if constexpr ((Mode & kMapXcdBlock) != 0) {  // XCD x: 64-channel blocks x, x + 8, ... (C % 512 == 0)
+    const int xcd = item & 7, local = (item >> 3) % (P.B * (P.C >> 3));
+    const int cl = local % (P.C >> 3);
+    b = local / (P.C >> 3);
+    c = ((cl >> 6) * 8 + xcd) * 64 + (cl & 63);
   } else if constexpr ((Mode & kMapXcdFlat) != 0) {  // XCD x: items [x B C/8, (x+1) B C/8) of the (b, c) order
     const int xcd = item & 7, local = (item >> 3) % (P.B * (P.C >> 3));
     const int flat = xcd * (P.B * (P.C >> 3)) + local;
@@ -1500,6 +1505,7 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 262144: return bf::launch_i8_item<true, 2, true, 262144>(P, st);
       case 524288: return bf::launch_i8_item<true, 2, true, 524288>(P, st);
       case 4194304: return bf::launch_i8_item<true, 2, true, 4194304>(P, st);
+      case 8388608: return bf::launch_i8_item<true, 2, true, 8388608>(P, st);
       case 1048576: return bf::launch_i8_item<true, 2, true, 1048576>(P, st);
       case 2097152: return bf::launch_i8_item<true, 2, true, 2097152>(P, st);  // channel fastest (earlier order)
       case 65536: return bf::launch_i8_item<true, 2, true, 65536>(P, st);

@@ -99,7 +99,7 @@ names_i8 = {0: "full (fast+fixup coef, occ 3)", 128: "exact-only coef", 16: "fas
             5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
             65: "occ 2, no-store", 1024: "serial coef", 2048: "pol order", 3072: "serial+pol order",
             4096: "occ4 (spills)", 7168: "occ4 serial+pol", 6144: "occ4 pol order",
-            262144: "batch-fastest order", 524288: "xcd x batch order", 1048576: "xcd range, batch fast", 2097152: "channel-fastest (old)", 4194304: "xcd flat (b, c)", 65536: "prio while loading", 131072: "prio while storing", 8192: "plain stores", 16384: "plain loads", 24576: "plain loads+stores"}
+            262144: "batch-fastest order", 524288: "xcd x batch order", 1048576: "xcd range, batch fast", 2097152: "channel-fastest (old)", 4194304: "xcd flat (b, c)", 8388608: "xcd 64-ch blocks", 65536: "prio while loading", 131072: "prio while storing", 8192: "plain stores", 16384: "plain loads", 24576: "plain loads+stores"}
 alg_i8 = nin + nout // 4
 if _os.environ.get("I8_AB"):  # interleaved A/B: int8 item kernel with uniform-base (A == 64) vs clamped addressing
     ab = {"uniform": [], "clamped": []}
