@@ -10,16 +10,22 @@
 // per iteration).  For A % 8 == 0 a thread reads the 8 antennas' dwords of one time sample (both pols) and splits
 // them with v_perm into the two pols' outputs; other A use 2-byte transposed reads.  The odd dword pitch (TT + 1)
 // keeps the transposed LDS reads (nearly) bank-conflict-free.
+#include <cstdlib>
+
 #include "bf_common.hpp"
 
 namespace bf {
 
 template <bool Oct>
 __global__ __launch_bounds__(256) void reorder_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                      int A, int C, int T, int TT, int nchunk) {
+                                                      int A, int C, int T, int TT, int nchunk, int xcd_range) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_u32[];
-  const int chunk = blockIdx.x % nchunk;
-  const long long bc = blockIdx.x / nchunk;
+  // XCD-range order (grid % 8 == 0): workgroups are dealt round-robin to the 8 XCDs, so XCD x takes the contiguous
+  // tile range [x N/8, (x+1) N/8) and streams one contiguous window per antenna (as the fused item kernels)
+  const long long tile = xcd_range ? (blockIdx.x & 7) * static_cast<long long>(gridDim.x >> 3) + (blockIdx.x >> 3)
+                                   : static_cast<long long>(blockIdx.x);
+  const int chunk = static_cast<int>(tile % nchunk);
+  const long long bc = tile / nchunk;
   const long long b = bc / C;
   const int c = static_cast<int>(bc % C);
   const int t0 = chunk * TT;
@@ -130,12 +136,14 @@ extern "C" int bf_reorder(const uint8_t* in, uint8_t* out, int B, int A, int C, 
   const long long grid = static_cast<long long>(B) * C * nchunk;
   BF_REQUIRE(grid < (1LL << 31), "bf_reorder: grid too large");
   const size_t lds = static_cast<size_t>(A) * (TT + 1) * 4;
+  const char* e = getenv("BF_REORDER_ORDER");  // measurement: "channel" keeps the plain order
+  const int xcd_range = grid % 8 == 0 && !(e && e[0] == 'c');
   if (A % 8 == 0) {
     hipLaunchKernelGGL(bf::reorder_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(256), lds,
-                       bf::as_stream(stream), in, out, A, C, T, TT, nchunk);
+                       bf::as_stream(stream), in, out, A, C, T, TT, nchunk, xcd_range);
   } else {
     hipLaunchKernelGGL(bf::reorder_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(256), lds,
-                       bf::as_stream(stream), in, out, A, C, T, TT, nchunk);
+                       bf::as_stream(stream), in, out, A, C, T, TT, nchunk, xcd_range);
   }
   BF_LAUNCHED("reorder_kernel");
 }
