@@ -11,8 +11,24 @@ SRCS     := $(CSRC)/bf_runtime.cpp $(CSRC)/bf_coeff.hip $(CSRC)/bf_reorder.hip $
 OBJS     := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 HDRS     := $(wildcard $(CSRC)/*.hpp) include/bf.h
 
-.PHONY: all clean diag
-all: $(LIB)
+.PHONY: all clean diag cabi
+all: $(LIB) cabi
+
+# C callers of the ABI (tests/test_c_abi.py): the harness-order smoke and INTEGRATION.md's streaming example,
+# compiled from the markdown block itself.  Plain C against include/bf.h, linked to the in-tree libbf.so.
+CC       ?= gcc
+CABI     := build/bf_smoke build/bf_stream_doc
+cabi: $(CABI)
+build/stream_snippet.inc: INTEGRATION.md
+	@mkdir -p build
+	awk '/<!-- snippet: stream -->/{f=1; next} f && /^```c/{p=1; next} p && /^```/{exit} p' $< > $@
+	@test -s $@ || { echo "no stream snippet in INTEGRATION.md"; rm -f $@; exit 1; }
+build/bf_smoke: tests/c/bf_smoke.c include/bf.h $(LIB)
+	@mkdir -p build
+	$(CC) -std=c11 -O2 -Wall -Iinclude $< -o $@ -L$(dir $(LIB)) -lbf -lm -Wl,-rpath,'$$ORIGIN/../$(dir $(LIB))'
+build/bf_stream_doc: tests/c/bf_stream_doc.c build/stream_snippet.inc include/bf.h $(LIB)
+	@mkdir -p build
+	$(CC) -std=c11 -O2 -Wall -Iinclude -Ibuild $< -o $@ -L$(dir $(LIB)) -lbf -Wl,-rpath,'$$ORIGIN/../$(dir $(LIB))'
 
 build/%.o: $(CSRC)/% $(HDRS)
 	@mkdir -p build

@@ -1,6 +1,6 @@
 """Headline benchmark: int8 voltage Gsamples/s through the fused MI355X beamformer (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg2] [--no-cpu-baseline] [--no-pmc]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg2|cfg4] [--no-cpu-baseline] [--no-pmc]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
 A "step" is one pass of the hot path over one batch block of synthetic input already resident in HBM: one
@@ -8,14 +8,22 @@ A "step" is one pass of the hot path over one batch block of synthetic input alr
 delay model + the antenna x beam complex contraction, for every (batch, pol, channel, sample) of the shard.
 Workload cfg3 (default, BASELINE configs[2], the north-star target): 64 antennas, 16 beams, 4096 channels per
 GPU, T = 256 samples, B = 8 batches, dual-pol int8 voltages, int8 requantised beams from the integer MFMA path
-(bit-exact to the oracle's integer contract; `--output f32` gives float32 beams).  cfg2 (configs[1]): 1 beam.
-Frequency channels shard across ranks with no data-path collective (rank r = X-engine r, channels
-[4096 r, 4096 (r+1)) of a 4096*N-channel band): scaling is weak.
+(bit-exact to the oracle's integer contract; `--output f32` gives float32 beams, `--int8-contract f32` int8 beams
+requantised from the float32 path).  cfg2 (configs[1]): 1 beam.  cfg4 (configs[3], per GPU): 256 ants, 64 beams.
+
+Multi-GPU: frequency channels shard across ranks with no data-path collective (rank r = X-engine r,
+channels [C r, C (r+1)) of a C*N-channel band): scaling is weak.  The only collective is the root -> ranks channel
+scatter of the full-band voltage cube, over RCCL (`torch.distributed` backend "nccl") on the GPUs: rank 0 builds
+the band in its HBM, packs each rank's channel slice contiguously and scatters it; each rank's timed hot path then
+runs on the slice it received.  The scatter is timed on its own (outside the hot-path timing) and reported in the
+line's `scatter` block.  The timing bracket (barrier + max over ranks) runs over gloo.
 
 Rank 0 prints ONE JSON line.  `value` = samples all ranks processed / max-over-ranks wall time of the K timed
 steps (barrier + device sync on both sides).  `roofline.achieved` = algorithmic bytes per launch / average
-launch duration from HIP events on the launch stream.  `roofline.traffic` = HBM bytes per launch from
-rocprofv3 PMC counters (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate passes), rank 0, N = 1.
+launch duration from HIP events on the launch stream; `roofline.read_frac` = the voltage bytes alone / that time /
+peak (the north star's "HBM-read roofline").  `roofline.traffic` = HBM bytes per launch from rocprofv3 PMC
+counters (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate passes), rank 0, N = 1.  `ceiling` = the same
+traffic mix as a plain streaming kernel on this box (diagnostic library), when it is built.
 `cpu_baseline` = the oracle's vectorised NumPy restatement on a bounded channel sample, rank 0, N = 1.
 """
 import argparse
@@ -32,7 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "int8 voltage Gsamples/s ingested + beams/s, 64-ant 4096-ch; % HBM roofline"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6290 measured float4 copy
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 TS = 1 / 1712e6
 
 WORKLOADS = {
@@ -54,15 +62,22 @@ def parse():
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
     p.add_argument("--output", choices=("int8", "f32"), default="int8",
                    help="int8 requantised beams (bit-exact integer path, default) or float32 beams")
+    p.add_argument("--int8-contract", choices=("q14", "f32"), default="q14",
+                   help="int8 beams from the Q14 integer path (default) or requantised from the float32 path")
     p.add_argument("--out-int8", action="store_true", help="same as --output int8")
     p.add_argument("--out-f32", action="store_true", help="same as --output f32")
     p.add_argument("--settle-ms", type=float, default=300.0,
                    help="untimed clock-settle launches after the warmup steps (milliseconds of wall time)")
     p.add_argument("--unsigned", action="store_true", help="uint8 voltages (the reference slots' dtype) instead of int8")
     p.add_argument("--nbuf", type=int, default=2, help="rotating input/output buffer sets (defeat the 256 MB MALL)")
+    p.add_argument("--scatter-backend", choices=("nccl", "gloo", "none"), default="nccl",
+                   help="N > 1: how the full-band cube reaches the ranks (nccl = RCCL over xGMI, device to device; "
+                        "gloo = host staging, for rehearsals with several ranks on one GPU; none = per-rank "
+                        "synthetic input)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-secondary", action="store_true")
+    p.add_argument("--no-ceiling", action="store_true")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args()
     if a.out_f32:
@@ -74,20 +89,28 @@ def parse():
 
 
 class Dist:
-    """Barrier + max-reduction across ranks (gloo, CPU): the timing bracket only; no data-path collective."""
+    """Barrier + max-reduction across ranks (gloo, CPU) for the timing bracket, plus an RCCL group for the
+    channel scatter.  torch is imported before libbf, so one HIP runtime serves both (its libamdhip64 SONAME is
+    the one libbf.so links)."""
 
-    def __init__(self):
+    def __init__(self, scatter_backend="none"):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.dist = None
+        self.scatter_backend = scatter_backend if self.world > 1 else "none"
+        self.nccl = None
         if self.world > 1:
-            import torch.distributed as dist  # imported before libbf so one HIP runtime serves both
+            import torch
+            import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             saved = os.dup(1)  # gloo prints its connection banner on stdout: keep stdout for the JSON line
             os.dup2(2, 1)
             try:
                 dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+                if self.scatter_backend == "nccl":
+                    torch.cuda.set_device(self.local_rank % max(torch.cuda.device_count(), 1))
+                    self.nccl = dist.new_group(backend="nccl")
                 dist.barrier()
             finally:
                 sys.stdout.flush()
@@ -113,41 +136,127 @@ class Dist:
 
 
 def make_inputs(np, rng, shape, nbuf, unsigned=False):
-    if unsigned:
-        return [rng.integers(0, 256, size=shape, dtype=np.uint8) for _ in range(nbuf)]
-    return [rng.integers(-128, 128, size=shape, dtype=np.int8) for _ in range(nbuf)]
+    n = int(np.prod(shape))
+    return [np.frombuffer(rng.bytes(n), np.uint8 if unsigned else np.int8).reshape(shape) for _ in range(nbuf)]
 
 
-def run_gpu(args, dist, wl):
+def scatter_inputs(args, dist, shape):
+    """The channel scatter: rank 0 holds the full band (B, A, C*N, T, 2, 2) and sends rank r its
+    packed channel slice [C r, C (r+1)).  Returns (per-rank slice, report).  nccl: device tensors over RCCL (the
+    band is generated in rank 0's HBM); gloo: host arrays (rehearsal).  The slice is what this rank's timed hot
+    path then processes."""
     import numpy as np
+    import torch
 
-    from dpdk_dc_sand_amd import _lib, accel
+    from dpdk_dc_sand_amd.shard import pack_channel_slices
+
+    B, A, C, T = shape[:4]
+    world, rank = dist.world, dist.rank
+    per_rank = int(np.prod(shape))
+    tdt = torch.uint8 if args.unsigned else torch.int8
+    report = {"backend": dist.scatter_backend, "bytes_per_rank": per_rank, "ranks": world,
+              "band_shape": [B, A, C * world, T, 2, 2]}
+    if dist.scatter_backend == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+        parts = None
+        if rank == 0:
+            g = torch.Generator(device=dev)
+            g.manual_seed(1)
+            lo, hi = (0, 256) if args.unsigned else (-128, 128)
+            band = torch.randint(lo, hi, (B, A, C * world, T, 2, 2), dtype=tdt, device=dev, generator=g)
+            parts = [band[:, :, r * C:(r + 1) * C].contiguous() for r in range(world)]  # pack: B*A strided runs
+            del band
+        out = torch.empty(shape, dtype=tdt, device=dev)
+        warm = torch.ones(1, device=dev)
+        dist.dist.all_reduce(warm, group=dist.nccl)  # communicator set-up outside the timing
+        times = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            dist.dist.scatter(out, scatter_list=parts, src=0, group=dist.nccl)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        del parts
+        t = dist.max(min(times))
+        report["collective"] = "RCCL scatter (torch.distributed nccl) over xGMI, device to device"
+    else:
+        full = None
+        if rank == 0:
+            rng = np.random.default_rng(1)
+            n = B * A * C * world * T * 4
+            full = np.frombuffer(rng.bytes(n), np.uint8 if args.unsigned else np.int8).reshape(
+                B, A, C * world, T, 2, 2)
+        dist.barrier()
+        t0 = time.perf_counter()
+        ttype = torch.from_numpy(np.zeros(1, np.uint8 if args.unsigned else np.int8)).dtype
+        out = torch.empty(shape, dtype=ttype)
+        if rank == 0:
+            dist.dist.scatter(out, scatter_list=[torch.from_numpy(p) for p in pack_channel_slices(full, world)], src=0)
+        else:
+            dist.dist.scatter(out, src=0)
+        t = dist.max(time.perf_counter() - t0)
+        out = out.numpy()
+        report["collective"] = "gloo scatter through host memory (rehearsal backend)"
+    report["seconds"] = round(t, 6)
+    report["GBps_per_peer"] = round(per_rank / t / 1e9, 2)
+    report["GBps_root_egress"] = round(per_rank * (world - 1) / t / 1e9, 2)
+    return out, report
+
+
+def template(args, dist, wl, int8_contract=None, kernel_path="auto"):
     from dpdk_dc_sand_amd.beamforming import FusedBeamformerTemplate
-
-    n_dev = accel.device_count()
-    if n_dev < 1:
-        raise RuntimeError("no HIP device visible")
-    ctx = accel.create_some_context(device=dist.local_rank % n_dev)
-    queue = ctx.create_command_queue()
     A, M, C, T, B = wl["A"], wl["M"], wl["C"], wl["T"], wl["B"]
     Ctot = wl.get("Ctot", C * max(dist.world, 1))
-    tmpl = FusedBeamformerTemplate(ctx, B, C, Ctot, T, A, M, xeng_id=dist.rank, sample_period=TS, delay_channels=1,
-                                   sample_signed=not args.unsigned, out_int8=args.out_int8, out_scale=1 / 64,
-                                   t0=0.0, batch_dt=T * 2 * Ctot * TS)
-    rng = np.random.default_rng(1 + dist.rank)
-    d = np.zeros(tmpl.delay_shape, np.float32)  # compact (1, M, A, 4) polynomial delay model with rates
+    return FusedBeamformerTemplate(args.ctx, B, C, Ctot, T, A, M, xeng_id=dist.rank, sample_period=TS,
+                                   delay_channels=1, sample_signed=not args.unsigned, out_int8=args.out_int8,
+                                   out_scale=1 / 64, t0=0.0, batch_dt=T * 2 * Ctot * TS,
+                                   int8_contract=int8_contract or args.int8_contract, kernel_path=kernel_path)
+
+
+def delay_model(np, rng, shape):
+    d = np.zeros(shape, np.float32)  # compact (1, M, A, 4) polynomial delay model with rates
     d[..., 0] = rng.uniform(0, 10 * TS, d.shape[:-1])
     d[..., 1] = rng.uniform(-1e-9, 1e-9, d.shape[:-1])
     d[..., 2] = rng.uniform(-np.pi, np.pi, d.shape[:-1])
     d[..., 3] = rng.uniform(-1, 1, d.shape[:-1])
+    return d
+
+
+def run_gpu(args, dist, wl, tmpl=None, inputs=None):
+    """Time K launches of the fused operator.  `inputs`: this rank's resident input (a torch device tensor from
+    the RCCL scatter, or a host array), else synthetic host data."""
+    import numpy as np
+
+    from dpdk_dc_sand_amd import accel
+
+    queue = args.queue
+    tmpl = tmpl or template(args, dist, wl)
+    rng = np.random.default_rng(1 + dist.rank)
+    d = delay_model(np, rng, tmpl.delay_shape)
     ops = []
-    for i, host in enumerate(make_inputs(np, rng, tmpl.input_shape, args.nbuf, args.unsigned)):
+    hosts = None
+    if inputs is None:
+        hosts = make_inputs(np, rng, tmpl.input_shape, args.nbuf, args.unsigned)
+    for i in range(args.nbuf):
         op = tmpl.instantiate(queue)
+        if inputs is not None and hasattr(inputs, "data_ptr"):
+            # the scattered device tensor itself for buffer 0, a device-side copy for the others
+            src = inputs if i == 0 else inputs.clone()
+            op.bind(inSamples=accel.DeviceArray(args.ctx, tmpl.input_shape, op.slots["inSamples"].dtype,
+                                                ptr=src.data_ptr(), owner=False))
+            op._keep = src
         op.ensure_all_bound()
-        op.buffer("inSamples").set(queue, host)
+        if hosts is not None:
+            op.buffer("inSamples").set(queue, hosts[i])
+        elif not hasattr(inputs, "data_ptr"):
+            op.buffer("inSamples").set(queue, inputs)
         op.buffer("delay_vals").set(queue, d)
         ops.append(op)
-    del host
+    del hosts
+    if inputs is not None and hasattr(inputs, "data_ptr"):
+        import torch
+        torch.cuda.synchronize()  # the clones are on torch's stream
     for i in range(args.warmup):
         ops[i % len(ops)]()
     queue.finish()
@@ -175,11 +284,67 @@ def run_gpu(args, dist, wl):
     dist.barrier()
     kernel_s = e1.time_since(e0) / args.steps
     t_max = dist.max(t_local)
-    samples_per_step = A * 2 * C * T * B  # complex 8-bit samples (ant, pol, chan, time, batch)
-    beams_per_step = M * 2 * C * T * B
-    return dict(t_max=t_max, kernel_s=kernel_s, samples_per_step=samples_per_step, beams_per_step=beams_per_step,
-                alg_bytes=tmpl.algorithmic_bytes(), device=ctx.device.name,
-                out=(ops, queue))
+    A, M, C, T, B = wl["A"], wl["M"], wl["C"], wl["T"], wl["B"]
+    return dict(t_max=t_max, kernel_s=kernel_s, samples_per_step=A * 2 * C * T * B, beams_per_step=M * 2 * C * T * B,
+                alg_bytes=tmpl.algorithmic_bytes(), read_bytes=A * 2 * C * T * B * 2, ops=ops, tmpl=tmpl, delays=d)
+
+
+def contract_check(args, dist, wl, r):
+    """Q14 integer contract vs requantise(float32 beams) on the headline's own input: the cost of the integer
+    contract in output values (at most one LSB by construction; the rate is measured here)."""
+    import numpy as np
+    op = r["ops"][0]
+    op()
+    args.queue.finish()
+    q14 = op.buffer("outData").get(args.queue)
+    alt = template(args, dist, wl, int8_contract="f32").instantiate(args.queue)
+    alt.bind(inSamples=op.buffer("inSamples"), delay_vals=op.buffer("delay_vals"))
+    alt.ensure_all_bound()
+    alt()
+    qf = alt.buffer("outData").get(args.queue)
+    diff = np.abs(q14.astype(np.int16) - qf.astype(np.int16))
+    return {"compared": "Q14 integer int8 beams vs int8 requantised from the float32 path, same input",
+            "values": int(diff.size), "mismatch_rate": float(np.count_nonzero(diff)) / diff.size,
+            "max_abs_lsb": int(diff.max())}
+
+
+def stream_ceiling(args, in_bytes, out_bytes):
+    """The same traffic mix (in_bytes read, out_bytes written) as plain streaming kernels from the diagnostic
+    library (build/libbf_diag.so: 16-byte lanes, plain / non-temporal loads and stores, 4:1 interleaved mix for
+    the int8 path): the best of them is this box's achievable ceiling for the fused kernel's traffic."""
+    import ctypes
+
+    from dpdk_dc_sand_amd import accel
+    path = os.path.join(ROOT, "build", "libbf_diag.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    V, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    lib.bf_diag_stream.argtypes = [V, V, S, S, I, I, V]
+    bufs = [(accel.DeviceArray(args.ctx, (in_bytes,), "u1"), accel.DeviceArray(args.ctx, (max(out_bytes, 16),), "u1"))
+            for _ in range(2)]
+    best = None
+    codes = [1, 101, 102, 103]
+    if out_bytes * 4 == in_bytes:
+        codes += [200, 201]
+    for grid in (1024, 2048):
+        for code in codes:
+            for i in range(3):
+                lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, in_bytes, out_bytes, grid, code,
+                                   args.queue.handle)
+            e0 = accel.Event(args.queue)
+            n = 10
+            for i in range(n):
+                lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, in_bytes, out_bytes, grid, code,
+                                   args.queue.handle)
+            e1 = accel.Event(args.queue)
+            args.queue.finish()
+            t = e1.time_since(e0) / n
+            if best is None or t < best[0]:
+                best = (t, grid, code)
+    return {"us": round(best[0] * 1e6, 2), "GBps": round((in_bytes + out_bytes) / best[0] / 1e9, 1),
+            "kernel": f"bf_diag_stream grid {best[1]} mode {best[2]}",
+            "note": "best plain streaming kernel over the same read/write byte mix on this box"}
 
 
 def cpu_baseline(wl, out_int8, seconds=10.0):
@@ -230,8 +395,8 @@ def pmc_traffic(args):
         out = tempfile.mkdtemp(prefix="bfpmc_", dir=os.environ.get("TMPDIR", "/tmp"))
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
-               "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--output", args.output] + \
-              (["--unsigned"] if args.unsigned else [])
+               "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--output", args.output,
+               "--int8-contract", args.int8_contract] + (["--unsigned"] if args.unsigned else [])
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
         if r.returncode != 0 or not files:
@@ -248,59 +413,81 @@ def pmc_traffic(args):
     return traffic, vals
 
 
-KERNELS = {False: ("beamform_fused_item_kernel",
-                  "f16 hi/lo-split coefficients on v_mfma_f32_16x16x32_f16, f32 accumulation"),
-           True: ("beamform_fused_i8_item_kernel",
-                  "Q14 two-limb int8 coefficients on v_mfma_i32_16x16x64_i8, exact int32 accumulation, int8 beams")}
+def compute_desc(out_int8, int8_contract):
+    if out_int8 and int8_contract == "q14":
+        return "Q14 two-limb int8 coefficients on v_mfma_i32_16x16x64_i8, exact int32 accumulation, int8 beams"
+    desc = "f16 hi/lo-split coefficients on v_mfma_f32_16x16x32_f16, f32 accumulation"
+    return desc + (", int8 beams requantised in-kernel from the float32 beams" if out_int8 else ", float32 beams")
 
 
-MFMA_PEAK = {True: (5000.0, "TOPS", "v_mfma_i32_16x16x64_i8 (2x the dense BF16 rate, MI355X_MICROARCH.md)"),
-             False: (2500.0, "TFLOP/s", "v_mfma_f32_16x16x32_f16 (dense F16 = BF16 rate)")}
-
-
-def mfma_util(wl, out_int8, kernel_s):
+def mfma_util(wl, out_int8, int8_contract, kernel_s):
     """Matrix-core utilisation of the dominant kernel: algorithmic ops (8 A M per (b, p, c, t): the complex MAC)
     and the ops the MFMAs actually issue (two coefficient limbs, K = 2A padded to the MFMA depth, N = 2M padded
     to 16), both against the dense peak.  The path is HBM-bound by design (SURVEY §7 hard part 1): this shows the
     headroom, not a target."""
     A, M, C, T, B = wl["A"], wl["M"], wl["C"], wl["T"], wl["B"]
-    kg = 64 if out_int8 else 32
+    integer = out_int8 and int8_contract == "q14"
+    kg = 64 if integer else 32
     kpad, npad = -(-2 * A // kg) * kg, -(-2 * M // 16) * 16
     alg = 8.0 * A * M * 2 * C * T * B
     issued = 2.0 * 2 * kpad * npad * T * 2 * C * B
-    peak, unit, instr = MFMA_PEAK[out_int8]
+    peak, unit, instr = ((5000.0, "TOPS", "v_mfma_i32_16x16x64_i8 (2x the dense BF16 rate, MI355X_MICROARCH.md)")
+                         if integer else (2500.0, "TFLOP/s", "v_mfma_f32_16x16x32_f16 (dense F16 = BF16 rate)"))
     return {"instruction": instr, "unit": unit, "peak": peak, "algorithmic": round(alg / kernel_s / 1e12, 1),
             "issued": round(issued / kernel_s / 1e12, 1), "frac_issued": round(issued / kernel_s / 1e12 / peak, 4)}
 
 
-def kernel_name(wl, out_int8):
+def kernel_name(wl, out_int8, int8_contract="q14"):
     """The launch's dominant kernel (bf_fused.hip dispatch): item kernels for A <= 64 and T <= 256, else the wide
-    kernel (f32 beams) / the generic integer kernel (int8 beams)."""
+    kernels."""
+    integer = out_int8 and int8_contract == "q14"
     if wl["A"] <= 64 and wl["T"] <= 256:
-        return KERNELS[out_int8][0]
-    return "beamform_fused_i8_wide_kernel" if out_int8 else "beamform_fused_wide_kernel"
+        return "beamform_fused_i8_item_kernel" if integer else "beamform_fused_item_kernel"
+    return "beamform_fused_i8_wide_kernel" if integer else "beamform_fused_wide_kernel"
 
 
-def secondary(args, dist, workload, out_int8):
-    sub = argparse.Namespace(**{**vars(args), "workload": workload, "out_int8": out_int8})
-    r = run_gpu(sub, dist, WORKLOADS[workload])
-    r.pop("out")
-    return {"workload": workload + ": " + WORKLOADS[workload]["desc"], "output": "int8" if out_int8 else "float32",
-            "kernel": kernel_name(WORKLOADS[workload], out_int8),
-            "value": round(r["samples_per_step"] * args.steps / r["t_max"] / 1e9, 2), "unit": "Gsamples/s",
-            "roofline_frac": round(r["alg_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
-            "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"]}
+def secondary(args, dist, workload, out_int8, int8_contract="q14"):
+    sub = argparse.Namespace(**{**vars(args), "workload": workload, "out_int8": out_int8,
+                                "int8_contract": int8_contract})
+    wl = WORKLOADS[workload]
+    r = run_gpu(sub, dist, wl)
+    r.pop("ops")
+    out = {"workload": workload + ": " + wl["desc"],
+           "output": ("int8" + ("" if int8_contract == "q14" else " (requantised from float32 beams)"))
+           if out_int8 else "float32",
+           "kernel": kernel_name(wl, out_int8, int8_contract),
+           "value": round(r["samples_per_step"] * args.steps / r["t_max"] / 1e9, 2), "unit": "Gsamples/s",
+           "roofline_frac": round(r["alg_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
+           "read_frac": round(r["read_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
+           "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"]}
+    if not args.no_ceiling:
+        ceil = stream_ceiling(args, r["read_bytes"], int(r["alg_bytes"] - r["read_bytes"]))
+        if ceil:
+            out["ceiling"] = ceil
+            out["frac_of_ceiling"] = round(ceil["us"] / out["avg_launch_us"], 4)
+    return out
 
 
 def main():
     args = parse()
     wl = WORKLOADS[args.workload]
-    dist = Dist()
+    dist = Dist(args.scatter_backend)
+    from dpdk_dc_sand_amd import accel
+
+    n_dev = accel.device_count()
+    if n_dev < 1:
+        raise RuntimeError("no HIP device visible")
+    args.ctx = accel.create_some_context(device=dist.local_rank % n_dev)
+    args.queue = args.ctx.create_command_queue()
     if args.pmc_child:
         run_gpu(args, dist, wl)
         return
-    r = run_gpu(args, dist, wl)
-    ops_queue = r.pop("out")
+    tmpl = template(args, dist, wl)
+    scatter = None
+    inputs = None
+    if dist.world > 1 and dist.scatter_backend != "none":
+        inputs, scatter = scatter_inputs(args, dist, tmpl.input_shape)
+    r = run_gpu(args, dist, wl, tmpl=tmpl, inputs=inputs)
     total_samples = r["samples_per_step"] * args.steps * dist.world
     value = total_samples / r["t_max"] / 1e9
     achieved = r["alg_bytes"] / r["kernel_s"] / 1e9
@@ -312,24 +499,40 @@ def main():
         "config": {"workload": args.workload + ": " + wl["desc"], "n_ants": wl["A"], "n_beams": wl["M"],
                    "n_channels_per_gpu": wl["C"], "n_samples_per_channel": wl["T"], "n_batches": wl["B"],
                    "n_pols": 2, "output": "int8" if args.out_int8 else "float32",
+                   "int8_contract": args.int8_contract if args.out_int8 else None,
                    "parallelism": f"channel-shard x{dist.world} (xeng_id = rank), no data-path collective"},
         "beams_per_s": round(r["beams_per_step"] * args.steps * dist.world / r["t_max"], 1),
-        "compute": KERNELS[args.out_int8][1],
-        "device": r["device"],
+        "compute": compute_desc(args.out_int8, args.int8_contract),
+        "device": args.ctx.device.name,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": kernel_name(wl, args.out_int8), "avg_launch_us": round(r["kernel_s"] * 1e6, 2),
-                     "alg_bytes_per_launch": r["alg_bytes"]},
-        "mfma": mfma_util(wl, args.out_int8, r["kernel_s"]),
+                     "read_frac": round(r["read_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
+                     "kernel": kernel_name(wl, args.out_int8, args.int8_contract),
+                     "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"],
+                     "read_bytes_per_launch": r["read_bytes"]},
+        "mfma": mfma_util(wl, args.out_int8, args.int8_contract, r["kernel_s"]),
+        "scatter": scatter or {"backend": None, "note": "no scatter: single rank, or --scatter-backend none "
+                                                        "(each rank generates its shard in place)"},
         "cpu_baseline": None,
     }
-    del ops_queue
+    if dist.rank == 0 and dist.world == 1 and args.out_int8 and args.int8_contract == "q14":
+        line["int8_contract_check"] = contract_check(args, dist, wl, r)
+    r.pop("ops")
+    if dist.rank == 0 and dist.world == 1 and not args.no_ceiling:
+        ceil = stream_ceiling(args, r["read_bytes"], int(r["alg_bytes"] - r["read_bytes"]))
+        if ceil:
+            line["ceiling"] = ceil
+            line["roofline"]["frac_of_ceiling"] = round(ceil["us"] / line["roofline"]["avg_launch_us"], 4)
     if dist.rank == 0 and dist.world == 1 and not args.no_secondary and args.workload == "cfg3":
         line["secondary"] = []
-        for workload, out_int8 in (("cfg2", args.out_int8), ("cfg3", not args.out_int8), ("cfg4", args.out_int8),
-                                   ("cfg4", not args.out_int8)):
+        cases = [("cfg2", args.out_int8, "q14"), ("cfg3", not args.out_int8, "q14"), ("cfg3", True, "f32"),
+                 ("cfg4", True, "q14"), ("cfg4", False, "q14")]
+        for workload, out_int8, contract in cases:
+            if (workload, out_int8, contract if out_int8 else "q14") == (args.workload, args.out_int8,
+                                                                          args.int8_contract if args.out_int8 else "q14"):
+                continue
             try:
-                line["secondary"].append(secondary(args, dist, workload, out_int8))
+                line["secondary"].append(secondary(args, dist, workload, out_int8, contract))
             except Exception as e:  # secondary lines are informational
                 line["secondary"].append({"workload": workload, "error": str(e)[:200]})
     if dist.rank == 0 and dist.world == 1 and not args.no_pmc:

@@ -37,13 +37,23 @@ class FusedBeamformerTemplate:
     exact_coeffs: float64 phasors bit-exact to CoeffGenerator (then, with zero rates, the output equals
         OpSequence's bit for bit); default False = float32 phasors within ~1 ulp, several times cheaper.
     beam_weights: carry a per-(beam, input) real weight table (slot beamWeights, set with set_beam_weights).
+    int8_contract: with out_int8, "q14" (default: the integer contract, Q14 coefficients and exact int32 sums on the
+        integer MFMA path) or "f32" (requantised float32 beams: the reference's float32 coefficient arithmetic).
+    kernel_path, workgroup_order: force a kernel path ("auto", "item", "pipe", "generic", "wide", "wide16") or
+        workgroup order ("auto", "channel", "xcd") -- tests and measurement; every path computes the same contract.
     """
+
+    # int32 bound of the Q14 contract: |Wc| + |Ws| <= sqrt(2) * 2^14 * |g| + 1 per coefficient
+    @staticmethod
+    def _int8_sum_bound(n_ants, signed, gain=1.0):
+        return n_ants * (128 if signed else 255) * (np.sqrt(2.0) * 16384.0 * gain + 1.0)
 
     def __init__(self, context, n_batches: int, n_channels_per_stream: int, n_channels: int,
                  n_samples_per_channel: int, n_ants: int, n_beams: int, xeng_id: int = 0,
                  sample_period: float = 1 / 1712e6, delay_channels=None, sample_signed: bool = False,
                  out_int8: bool = False, out_scale: float = 1.0, t0: float = 0.0, batch_dt: float = 0.0,
-                 exact_coeffs: bool = False, beam_weights: bool = False) -> None:
+                 exact_coeffs: bool = False, beam_weights: bool = False, int8_contract: str = "q14",
+                 kernel_path: str = "auto", workgroup_order: str = "auto") -> None:
         for name, v in dict(n_batches=n_batches, n_channels_per_stream=n_channels_per_stream, n_channels=n_channels,
                             n_samples_per_channel=n_samples_per_channel, n_ants=n_ants, n_beams=n_beams).items():
             if int(v) <= 0:
@@ -56,6 +66,15 @@ class FusedBeamformerTemplate:
             raise ValueError("delay_channels must be 1 or n_channels_per_stream")
         if not sample_period > 0:
             raise ValueError("sample_period must be > 0")
+        if int8_contract not in ("q14", "f32"):
+            raise ValueError(f"int8_contract must be 'q14' or 'f32', got {int8_contract!r}")
+        if kernel_path not in _lib.FUSED_PATH:
+            raise ValueError(f"kernel_path must be one of {sorted(_lib.FUSED_PATH)}, got {kernel_path!r}")
+        if workgroup_order not in _lib.FUSED_ORDER:
+            raise ValueError(f"workgroup_order must be one of {sorted(_lib.FUSED_ORDER)}, got {workgroup_order!r}")
+        if out_int8 and int8_contract == "q14" and self._int8_sum_bound(n_ants, sample_signed) >= 2 ** 31:
+            raise ValueError(f"{n_ants} antennas overflow the int8 path's int32 beam sums; use float beams or "
+                             "int8_contract='f32'")
         self.context = context
         self.n_batches = n_batches
         self.n_pols = 2
@@ -76,8 +95,13 @@ class FusedBeamformerTemplate:
         self.batch_dt = float(batch_dt)
         self.exact_coeffs = bool(exact_coeffs)
         self.beam_weights = bool(beam_weights)
+        self.int8_contract = int8_contract
+        self.kernel_path = kernel_path
+        self.workgroup_order = workgroup_order
         self.flags = ((_lib.FUSED_SIGNED if self.sample_signed else 0) | (_lib.FUSED_OUT_INT8 if self.out_int8 else 0)
-                      | (_lib.FUSED_EXACT_COEFF if self.exact_coeffs else 0))
+                      | (_lib.FUSED_EXACT_COEFF if self.exact_coeffs else 0)
+                      | (_lib.FUSED_INT8_VIA_F32 if self.out_int8 and int8_contract == "f32" else 0)
+                      | _lib.FUSED_PATH[kernel_path] | _lib.FUSED_ORDER[workgroup_order])
         B, C, T, A, M = n_batches, n_channels_per_stream, n_samples_per_channel, n_ants, n_beams
         self.input_shape = (B, A, C, T, 2, 2)
         self.delay_shape = (delay_channels, M, A, 4)
@@ -87,15 +111,16 @@ class FusedBeamformerTemplate:
     def check_weights(self, weights):
         """Validate an (M, A) weight table for this configuration; returns it as float32.  The int8 output's
         Q14 integer path needs rne(|g| * 2^14) <= 32639, i.e. |g| <= 1.992 (the high limb stays int8), and
-        2*A*max|g|*2^14*255 < 2^31 (no int32 overflow); the float path takes any finite weights."""
+        A * max|x| * (sqrt(2) * max|g| * 2^14 + 1) < 2^31 (no int32 overflow); the float path takes any finite
+        weights."""
         w = np.asarray(weights, np.float32)
         if w.shape != self.weights_shape:
             raise ValueError(f"beam weights must have shape {self.weights_shape}, got {w.shape}")
         if not np.all(np.isfinite(w)):
             raise ValueError("beam weights must be finite")
-        if self.out_int8:
+        if self.out_int8 and self.int8_contract == "q14":
             g = float(np.max(np.abs(w))) if w.size else 0.0
-            if np.rint(g * 16384) > 32639 or 2 * self.n_ants * g * 16384 * 255 >= 2 ** 31:
+            if np.rint(g * 16384) > 32639 or self._int8_sum_bound(self.n_ants, self.sample_signed, g) >= 2 ** 31:
                 raise ValueError(f"beam weight magnitude {g} out of range for int8 output with {self.n_ants} inputs")
         return w
 

@@ -251,7 +251,7 @@ int launch_ring(const uint8_t* x, const float* w, float* y, long long bpc, int N
 template <bool Signed, int NTS>
 int dispatch_vec(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                  hipStream_t st) {
-  const char* e = getenv("BF_TABLE_BASIC");  // tests: force the basic kernel
+  const char* e = diag_env("BF_TABLE_BASIC");  // tests: force the basic kernel
   if (A % 4 == 0 && !(e && e[0] == '1')) {
     // ring depth: the k-steps of a row, up to 16 (the steps are padded to a multiple of R); long rows only
     if (S >= 16 && coef_lds_bytes((S + 15) / 16 * 16, NTS) <= kMaxLds)
@@ -259,7 +259,7 @@ int dispatch_vec(const uint8_t* x, const float* w, float* y, long long bpc, int 
     if (S >= 8 && coef_lds_bytes((S + 7) / 8 * 8, NTS) <= kMaxLds)
       return launch_ring<Signed, NTS, 8>(x, w, y, bpc, NB, A, M, S, NT, st);
     // 4..7 k-steps (64 antennas: config 3): a 4-deep ring
-    const char* r4 = getenv("BF_TABLE_RING4");  // measurement: 0 keeps the basic kernel
+    const char* r4 = diag_env("BF_TABLE_RING4");  // measurement: 0 keeps the basic kernel
     if (S >= 4 && !(r4 && r4[0] == '0') && coef_lds_bytes((S + 3) / 4 * 4, NTS) <= kMaxLds)
       return launch_ring<Signed, NTS, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
   }

@@ -7,6 +7,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/bf.h"
@@ -45,6 +46,18 @@ inline int hip_fail(hipError_t e, const char* what) {
   } while (0)
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Measurement knobs (load forms, slab widths, launch orders) are read from the environment only in the diagnostic
+// build (`make diag`, -DBF_DIAG, used by tools/diag_*.py).  The product library never reads the environment: kernel
+// paths and contract switches are explicit bf_beamform_fused flags (include/bf.h).
+inline const char* diag_env(const char* name) {
+#ifdef BF_DIAG
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 constexpr int kSamplesPerBlock = 16;  // matrix_multiply.py:76 (128 // 8)
 

@@ -1147,11 +1147,10 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
 
 // Workgroup order of the item kernels (item_coords): XCD-range when C % 8 == 0 and the beams are at least 8 (config
 // 3: 450-461 -> 432-433 us); channel-fastest for one or two beams, whose read-dominated traffic measured no better
-// that way (config 2: 334-357 vs 332-340 us, profiles/r1_v8_order_bench_ab.txt).  BF_ITEM_ORDER=xcd|channel forces.
+// that way (config 2: 334-357 vs 332-340 us, profiles/r1_v8_order_bench_ab.txt).  BF_FUSED_ORDER_XCD / _CHANNEL force.
 bool item_xcd_order(const FusedArgs& P) {
-  const char* e = getenv("BF_ITEM_ORDER");
-  if (e && e[0] == 'c') return false;
-  if (e && e[0] == 'x') return (P.C & 7) == 0;
+  if (P.order == BF_FUSED_ORDER_CHANNEL) return false;
+  if (P.order == BF_FUSED_ORDER_XCD) return (P.C & 7) == 0;
   return (P.C & 7) == 0 && P.M >= 8;
 }
 
@@ -1162,7 +1161,7 @@ int launch_i8_item(FusedArgs P, hipStream_t st, size_t min_lds = 0) {
   const size_t lds = std::max<size_t>(static_cast<size_t>(2) * NTS * 2 * 64 * 16 + 4 * 32 * 4, min_lds);
   const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
   BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many items");
-  const char* ae = getenv("BF_I8_A64");  // measurement: 0 forces the clamped per-lane addressing
+  const char* ae = diag_env("BF_I8_A64");  // measurement: 0 forces the clamped per-lane addressing
   const bool a64 = P.A == 64 && 24ull * P.C * P.T * 4 + P.T * 4ull < (1ull << 32) && !(ae && ae[0] == '0');
   if (a64)
     hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ, true>),
@@ -1176,10 +1175,11 @@ int launch_i8_item(FusedArgs P, hipStream_t st, size_t min_lds = 0) {
 template <bool Signed>
 int launch_i8(FusedArgs P, hipStream_t st) {
   const int S8 = (2 * P.A + 63) / 64;
-  const int choice = fused_kernel_choice();
+  const int choice = fused_kernel_choice(P);
   const bool small = S8 <= 2 && P.T <= 256;
-  if ((choice == 3 || (choice == 0 && !small)) && i8_wide_fits(P)) return launch_i8_wide<Signed>(P, st);
-  if (small && choice != 2) {
+  if ((choice == BF_FUSED_PATH_WIDE || choice == BF_FUSED_PATH_WIDE16 || (choice == 0 && !small)) && i8_wide_fits(P))
+    return launch_i8_wide<Signed>(P, st);
+  if (small && choice != BF_FUSED_PATH_GENERIC) {
     const int M2 = 2 * P.M;
     if (P.NT >= 2) {
       if (M2 % 32 == 0) return launch_i8_item<Signed, 2, true>(P, st);
@@ -1204,20 +1204,6 @@ int launch_i8(FusedArgs P, hipStream_t st) {
                        lds_bytes(1), st, P);
   }
   BF_LAUNCHED("beamform_fused_i8_kernel");
-}
-
-// ---------------------------------------------------------------------------------------------------------
-// Kernel choice for A <= 64, T <= 256: BF_FUSED_KERNEL = item (default) | pipe | generic; BF_FUSED_GENERIC=1 is
-// shorthand for generic (tests run every path against the oracle).
-int fused_kernel_choice() {
-  const char* g = getenv("BF_FUSED_GENERIC");
-  if (g && g[0] == '1') return 2;
-  const char* e = getenv("BF_FUSED_KERNEL");
-  if (!e) return 0;
-  if (e[0] == 'p') return 1;
-  if (e[0] == 'g') return 2;
-  if (e[0] == 'w') return 3;
-  return 0;
 }
 
 template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
@@ -1256,8 +1242,7 @@ int launch_generic(FusedArgs P, hipStream_t st) {
   P.nslabs = (P.NT + NTS - 1) / NTS;
   const size_t lds = coef_lds_bytes(P.S, NTS);
   BF_REQUIRE(lds <= kMaxLds, "bf_beamform_fused: n_ants=%d too large", P.A);
-  const char* xo = getenv("BF_FUSED_XCD_ORDER");
-  P.xcd_order = P.nslabs > 1 && !(xo && xo[0] == '0');
+  P.xcd_order = P.nslabs > 1 && P.order != BF_FUSED_ORDER_CHANNEL;
   const long long items = static_cast<long long>(P.B) * P.C;
   const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
@@ -1268,16 +1253,17 @@ int launch_generic(FusedArgs P, hipStream_t st) {
 
 template <bool Signed, bool OutI8, bool Exact>
 int dispatch(FusedArgs P, hipStream_t st) {
-  const int choice = fused_kernel_choice();
+  const int choice = fused_kernel_choice(P);
   const bool small = P.S <= kGroup && P.T <= 256;
   if constexpr (!OutI8) {
     // many antennas x beams (config 4): the wide kernel keeps every beam of the item in one workgroup
-    const bool wide = (choice == 3) || (choice == 0 && P.M >= 24 && (!small || P.M > 32));
+    const bool wide = choice == BF_FUSED_PATH_WIDE || choice == BF_FUSED_PATH_WIDE16 ||
+                      (choice == 0 && P.M >= 24 && (!small || P.M > 32));
     if (wide && wide_fits(P)) return launch_wide<Signed, Exact>(P, st);
   }
-  if (small && choice != 2) {
+  if (small && choice != BF_FUSED_PATH_GENERIC) {
     const int M2 = 2 * P.M;
-    if (choice == 1) {
+    if (choice == BF_FUSED_PATH_PIPE) {
       if (P.NT >= 2) {
         if (M2 % 32 == 0) return launch_pipe<Signed, OutI8, 2, Exact, true>(P, st);
         return launch_pipe<Signed, OutI8, 2, Exact, false>(P, st);
@@ -1292,7 +1278,7 @@ int dispatch(FusedArgs P, hipStream_t st) {
     if (M2 == 16) return launch_item<Signed, OutI8, 1, Exact, true>(P, st);
     return launch_item<Signed, OutI8, 1, Exact, false>(P, st);
   }
-  const char* wn = getenv("BF_FUSED_GENERIC_NTS");  // measurement: force the slab width
+  const char* wn = diag_env("BF_FUSED_GENERIC_NTS");  // measurement: force the slab width
   const int want = wn ? atoi(wn) : 2;
   if (want >= 4 && P.NT >= 4 && coef_lds_bytes(P.S, 4) <= kMaxLds) return launch_generic<Signed, OutI8, 4, Exact>(P, st);
   if (want >= 2 && P.NT >= 2 && coef_lds_bytes(P.S, 2) <= kMaxLds) return launch_generic<Signed, OutI8, 2, Exact>(P, st);
@@ -1318,8 +1304,12 @@ extern "C" int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay
   BF_REQUIRE(T % bf::kSamplesPerBlock == 0, "bf_beamform_fused: n_samples_per_channel=%d must be a multiple of 16", T);
   BF_REQUIRE(delay_channels == 1 || delay_channels == C, "bf_beamform_fused: delay_channels must be 1 or C");
   BF_REQUIRE(sample_period > 0.0, "bf_beamform_fused: sample_period must be > 0");
-  BF_REQUIRE((flags & ~(BF_FUSED_SIGNED | BF_FUSED_OUT_INT8 | BF_FUSED_EXACT_COEFF)) == 0,
+  BF_REQUIRE((flags & ~(BF_FUSED_SIGNED | BF_FUSED_OUT_INT8 | BF_FUSED_EXACT_COEFF | BF_FUSED_INT8_VIA_F32 |
+                         BF_FUSED_PATH_MASK | BF_FUSED_ORDER_MASK)) == 0,
              "bf_beamform_fused: unknown flags 0x%x", flags);
+  BF_REQUIRE((flags & BF_FUSED_PATH_MASK) <= BF_FUSED_PATH_WIDE16, "bf_beamform_fused: unknown kernel path 0x%x",
+             flags & BF_FUSED_PATH_MASK);
+  BF_REQUIRE((flags & BF_FUSED_ORDER_MASK) != BF_FUSED_ORDER_MASK, "bf_beamform_fused: unknown workgroup order");
   BF_REQUIRE((reinterpret_cast<uintptr_t>(raw) & 15) == 0 && (reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 &&
                  (reinterpret_cast<uintptr_t>(y) & 15) == 0,
              "bf_beamform_fused: misaligned buffer");
@@ -1343,11 +1333,19 @@ extern "C" int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay
   P.t0 = t0;
   P.batch_dt = batch_dt;
   P.out_scale = out_scale;
+  P.path = flags & BF_FUSED_PATH_MASK;
+  P.order = flags & BF_FUSED_ORDER_MASK;
   hipStream_t st = bf::as_stream(stream);
   const bool sgn = flags & BF_FUSED_SIGNED, i8 = flags & BF_FUSED_OUT_INT8, ex = flags & BF_FUSED_EXACT_COEFF;
-  if (i8) {
-    const char* e = getenv("BF_FUSED_INT8_FLOAT");  // measurement: float path + requantise instead
-    if (!(e && e[0] == '1')) return sgn ? bf::launch_i8<true>(P, st) : bf::launch_i8<false>(P, st);
+  // int8 beams: the Q14 integer contract (default), or requantised float beams (BF_FUSED_INT8_VIA_F32)
+  if (i8 && !(flags & BF_FUSED_INT8_VIA_F32)) {
+    // The contract's int32 sum: |y| <= A * max|x| * (|Wc| + |Ws|) with |Wc| + |Ws| <= sqrt(2) * 2^14 + 1 = 23171 at
+    // unit gain.  Beyond that the int32 accumulators would wrap (the oracle sums in int64): refuse.  With gains the
+    // caller, which owns the weights, checks the bound (FusedBeamformerTemplate.check_weights).
+    BF_REQUIRE(gains || static_cast<double>(A) * (sgn ? 128 : 255) * 23171.0 < 2147483648.0,
+               "bf_beamform_fused: n_ants=%d overflows the int8 path's int32 beam sums (%s samples); use float beams "
+               "or BF_FUSED_INT8_VIA_F32", A, sgn ? "int8" : "uint8");
+    return sgn ? bf::launch_i8<true>(P, st) : bf::launch_i8<false>(P, st);
   }
   if (sgn) {
     if (i8) return ex ? bf::dispatch<true, true, true>(P, st) : bf::dispatch<true, true, false>(P, st);

@@ -16,6 +16,7 @@ struct FusedArgs {
   const float* gain;  // optional (M, A) real per-input beam weights (?beam-weights), folded into the phasors
   void* y;
   int delay_channels, B, C, T, A, M, S, NT, nslabs, xcd_order;
+  int path, order;  // BF_FUSED_PATH_* and BF_FUSED_ORDER_* bits of the launch flags (0 = automatic)
   long long base_ch;
   double ctot, ts, k, t0, batch_dt;
   float out_scale;
@@ -75,8 +76,8 @@ __device__ __forceinline__ void transpose_rows4(uint32_t (&v)[4]) {
   v[3] = d[1];
 }
 
-// BF_FUSED_KERNEL = item (default) | pipe | generic | wide; BF_FUSED_GENERIC=1 is shorthand for generic.
-int fused_kernel_choice();
+// Kernel-path override of a launch (flags & BF_FUSED_PATH_MASK): 0 automatic, else one of the BF_FUSED_PATH_* values.
+inline int fused_kernel_choice(const FusedArgs& P) { return P.path; }
 
 // Integer wide kernel (bf_wide_i8.hip): int8 beams for many antennas x beams.
 bool i8_wide_fits(const FusedArgs& P);

@@ -95,7 +95,8 @@ int bf_pipeline_create(bf_pipeline** out, int B, int C, int T, int A, int M, int
   BF_REQUIRE(delay_channels == 1 || delay_channels == C, "bf_pipeline_create: delay_channels must be 1 or C");
   BF_REQUIRE(depth >= 1 && depth <= 64, "bf_pipeline_create: depth=%d out of [1, 64]", depth);
   BF_REQUIRE(sample_period > 0.0, "bf_pipeline_create: sample_period must be > 0");
-  BF_REQUIRE((flags & ~(BF_FUSED_SIGNED | BF_FUSED_OUT_INT8 | BF_FUSED_EXACT_COEFF)) == 0,
+  BF_REQUIRE((flags & ~(BF_FUSED_SIGNED | BF_FUSED_OUT_INT8 | BF_FUSED_EXACT_COEFF | BF_FUSED_INT8_VIA_F32 |
+                         BF_FUSED_PATH_MASK | BF_FUSED_ORDER_MASK)) == 0,
              "bf_pipeline_create: unknown flags 0x%x", flags);
   auto* p = new bf_pipeline();
   p->B = B, p->C = C, p->T = T, p->A = A, p->M = M, p->Ctot = Ctot, p->xeng_id = xeng_id, p->flags = flags;

@@ -136,7 +136,7 @@ extern "C" int bf_reorder(const uint8_t* in, uint8_t* out, int B, int A, int C, 
   const long long grid = static_cast<long long>(B) * C * nchunk;
   BF_REQUIRE(grid < (1LL << 31), "bf_reorder: grid too large");
   const size_t lds = static_cast<size_t>(A) * (TT + 1) * 4;
-  const char* e = getenv("BF_REORDER_ORDER");  // measurement: "channel" keeps the plain order
+  const char* e = bf::diag_env("BF_REORDER_ORDER");  // measurement: "channel" keeps the plain order
   const int xcd_range = grid % 8 == 0 && !(e && e[0] == 'c');
   if (A % 8 == 0) {
     hipLaunchKernelGGL(bf::reorder_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(256), lds,

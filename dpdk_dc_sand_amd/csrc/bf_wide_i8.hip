@@ -309,15 +309,14 @@ int launch_w8(FusedArgs P, hipStream_t st) {
   const size_t lds = static_cast<size_t>(Sp) * 2 * 2 * 64 * 16 + 4 * 32 * 4;
   BF_REQUIRE(lds <= kMaxLds, "bf_beamform_fused: n_ants=%d too large for the integer wide kernel", P.A);
   P.nslabs = (P.M + kW8Beams - 1) / kW8Beams;
-  const char* xo = getenv("BF_FUSED_XCD_ORDER");
-  P.xcd_order = P.nslabs > 1 && !(xo && xo[0] == '0');
+  P.xcd_order = P.nslabs > 1 && P.order != BF_FUSED_ORDER_CHANNEL;
   const long long items = static_cast<long long>(P.B) * P.C;
   const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
   // Buffer-resource loads (BF_W8_BUFFER=1, signed samples, in-item offsets below 2^31): the contraction alone runs
   // faster with them (no-coef/no-store 367 vs 394 us), the full kernel slower (609 vs 592 us, interleaved A/B,
   // profiles/r1_v7_w8_buffer_ab.txt), so the pointer form is the default.
-  const char* bo = getenv("BF_W8_BUFFER");
+  const char* bo = diag_env("BF_W8_BUFFER");
   const bool buf = Signed && static_cast<unsigned long long>(P.A) * P.C * P.T * 4 < (1ull << 31) &&
                    (bo && bo[0] == '1');
   if constexpr (Signed) {

@@ -108,10 +108,28 @@ int bf_beamform(const uint8_t* x, const float* w, float* y, int B, int P, int C,
  *                block of T samples, BeamformerParameters.h:17); with zero rates/dt it equals OpSequence
  *   y          : f32 (B, 2, C, T/16, 16, 2M), or int8 = sat127(rne(y * out_scale)) with BF_FUSED_OUT_INT8
  *   flags      : BF_FUSED_SIGNED (int8 samples), BF_FUSED_OUT_INT8, BF_FUSED_EXACT_COEFF (float64 phasors
- *                bit-exact to bf_coeff_gen; default is the ~1-ulp float32 fast phasor). */
+ *                bit-exact to bf_coeff_gen; default is the ~1-ulp float32 fast phasor).
+ * int8 beams have two contracts:
+ *   default               : the Q14 integer contract (oracle fused_beamform_int8): W = rne(2^14 * f32 phasor), exact
+ *                           int32 sums, q = sat127(rne(f32(y) * out_scale * 2^-14)); integer MFMA, bit-exact;
+ *   BF_FUSED_INT8_VIA_F32 : q = sat127(rne(y_f32 * out_scale)) of the float32 beams (the reference's float32
+ *                           coefficient arithmetic, requantised in-kernel == bf_requant of the float output).
+ * Kernel-path and workgroup-order overrides (BF_FUSED_PATH_*, BF_FUSED_ORDER_*) exist for tests and measurement:
+ * every path computes the same contract, a path that does not fit the shape falls through to one that does, and
+ * 0 (automatic) picks the fastest path for the shape.  The library never reads the environment. */
 #define BF_FUSED_SIGNED 1
 #define BF_FUSED_OUT_INT8 2
 #define BF_FUSED_EXACT_COEFF 4
+#define BF_FUSED_INT8_VIA_F32 8
+#define BF_FUSED_PATH_MASK 0x0f00
+#define BF_FUSED_PATH_ITEM 0x0100    /* one workgroup per (batch, channel) item (A <= 64, T <= 256), else generic */
+#define BF_FUSED_PATH_PIPE 0x0200    /* persistent double-buffered item kernel (float beams) */
+#define BF_FUSED_PATH_GENERIC 0x0300 /* any A, any T: groups of 64 antennas */
+#define BF_FUSED_PATH_WIDE 0x0400    /* many antennas x beams: multi-wave beam slabs (config 4) */
+#define BF_FUSED_PATH_WIDE16 0x0500  /* the float wide kernel with 16-beam slabs */
+#define BF_FUSED_ORDER_MASK 0x3000
+#define BF_FUSED_ORDER_CHANNEL 0x1000 /* plain channel-fastest workgroup order */
+#define BF_FUSED_ORDER_XCD 0x2000     /* XCD-range order (XCD x streams channels [x C/8, (x+1) C/8)) */
 int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, int delay_channels, void* y, int B, int C,
                       int T, int A, int M, int Ctot, int xeng_id, double sample_period, double t0,
                       double batch_dt, int flags, float out_scale, void* stream);
@@ -121,8 +139,9 @@ int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, int delay_cha
  * B-engines).  gains: f32 (M, A) real weight of antenna a in beam m on the device, or NULL (= all ones, exactly
  * bf_beamform_fused).  Coefficient (a, m) becomes (g*cos, g*sin), one float32 rounding per component.  With
  * BF_FUSED_OUT_INT8 the Q14 integer path needs |g| <= 1.992 (the high limb stays int8) and
- * 2*A*max|g|*2^14*255 < 2^31 (no int32 overflow); the Python wrapper, which owns the host copy of the weights,
- * checks both. */
+ * A*max|x|*(sqrt(2)*max|g|*2^14 + 1) < 2^31 (no int32 overflow; max|x| = 128 signed, 255 unsigned); the Python
+ * wrapper, which owns the host copy of the weights, checks both.  Without gains the library checks the unit-gain
+ * bound itself (A <= 363 unsigned, A <= 724 signed) and returns BF_ERR_ARG beyond it. */
 int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay_vals, int delay_channels, const float* gains,
                                void* y, int B, int C, int T, int A, int M, int Ctot, int xeng_id,
                                double sample_period, double t0, double batch_dt, int flags, float out_scale,

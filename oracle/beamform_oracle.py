@@ -18,7 +18,7 @@ def u8_voltages(shape, seed=2021):
     return rng.uniform(np.iinfo(np.uint8).min, np.iinfo(np.uint8).max, shape).astype(np.uint8)
 
 
-def coeff_rotation(delay_vals, C, Ctot, xeng_id, Ts, dt=0.0):
+def coeff_rotation(delay_vals, C, Ctot, xeng_id, Ts, dt=0.0, ch0=None):
     """Steering phase in float64, in the reference's exact left-to-right operation order.
 
     coeff_generator_cpu.py:125-164 (and coeff_generator.py:46-65):
@@ -30,6 +30,9 @@ def coeff_rotation(delay_vals, C, Ctot, xeng_id, Ts, dt=0.0):
     Time extension (used by the fused per-block regeneration): the delay and phase are
     first advanced by their rates, tau' = tau + tau_rate*dt and phi' = phi + phi_rate*dt, then the same
     expression is evaluated; at dt == 0 this is bit-identical to the reference.
+    ch0: absolute channel of row 0 when the rows are a slice of an engine's channels (default C * xeng_id, the
+    reference's `ichannel = c + C * xeng_id`, coeff_generator.py:53); lets tests check sampled channels of a
+    full-size launch.
     Returns float64 (C, M, A).
     """
     d = np.asarray(delay_vals, dtype=np.float32)
@@ -39,7 +42,8 @@ def coeff_rotation(delay_vals, C, Ctot, xeng_id, Ts, dt=0.0):
     if dt != 0.0:
         tau = tau + d[..., 1].astype(np.float64) * dt
         phi = phi + d[..., 3].astype(np.float64) * dt
-    ch = (np.arange(C, dtype=np.int64) + C * xeng_id).astype(np.float64)[:, None, None]
+    first = C * xeng_id if ch0 is None else int(ch0)
+    ch = (np.arange(C, dtype=np.int64) + first).astype(np.float64)[:, None, None]
     denom = float(Ctot) * Ts
     initial = tau * ch * (-math.pi) / denom + phi
     centre = tau * (Ctot / 2) * (-math.pi) / denom
@@ -80,10 +84,10 @@ def coeffs(delay_vals, B, P, C, Ctot, A, M, xeng_id, Ts=TS_MEERKAT):
     return _pack_blocks(cos, sin, B, P)
 
 
-def coeffs_at(delay_vals, C, Ctot, A, M, xeng_id, Ts, dt):
+def coeffs_at(delay_vals, C, Ctot, A, M, xeng_id, Ts, dt, ch0=None):
     """Compact complex coefficients at time offset dt: (cos, sin) f32, each (C, M, A)."""
     d = np.asarray(delay_vals, np.float32)
-    return _cos_sin_f32(coeff_rotation(d, C, Ctot, xeng_id, Ts, dt))
+    return _cos_sin_f32(coeff_rotation(d, C, Ctot, xeng_id, Ts, dt, ch0))
 
 
 def reorder(x):
@@ -118,19 +122,20 @@ def op_sequence(raw, delay_vals, C, Ctot, A, M, xeng_id=0, Ts=TS_MEERKAT):
     return complex_mult(reorder(raw), coeffs(delay_vals, B, 2, C, Ctot, A, M, xeng_id, Ts))
 
 
-def fused_beamform(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, signed=False, gains=None):
+def fused_beamform(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, signed=False, gains=None,
+                   ch0=None):
     """The fused MI355X operator's contract: reorder + per-batch coefficient regeneration + complex mult.
 
     raw: (B, A, C, T, 2, 2) 8-bit; delay_vals: (C, M, A, 4) or compact (1, M, A, 4) (same model for every
     channel).  Batch b uses coefficients at dt_b = t0 + b * batch_dt (the per-block regeneration of
     BeamformerParameters.h:17 ACCUMULATIONS_BEFORE_NEW_COEFFS).  gains: optional (M, A) real beam weights
-    (see fused_tables).  Output f32 (B, 2, C, T/16, 16, 2M)."""
+    (see fused_tables).  ch0: see coeff_rotation.  Output f32 (B, 2, C, T/16, 16, 2M)."""
     B, A, C, T, P, Z = raw.shape
-    w = fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt, gains)
+    w = fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt, gains, ch0)
     return complex_mult(reorder(raw), w, signed=signed)
 
 
-def fused_tables(delay_vals, B, C, Ctot, A, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, gains=None):
+def fused_tables(delay_vals, B, C, Ctot, A, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, gains=None, ch0=None):
     """The (B, 2, C, 2A, 2M) coefficient tables the fused operator applies (batch b at dt = t0 + b*batch_dt).
 
     gains: optional (M, A) float32 per-input beam weights (the `?beam-weights <beam> w_0..w_{A-1}` control request,
@@ -142,7 +147,7 @@ def fused_tables(delay_vals, B, C, Ctot, A, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, ba
     M = d.shape[1]
     w = np.empty((B, 2, C, 2 * A, 2 * M), np.float32)
     for b in range(B):
-        cos, sin = coeffs_at(d, C, Ctot, A, M, xeng_id, Ts, t0 + b * batch_dt)
+        cos, sin = coeffs_at(d, C, Ctot, A, M, xeng_id, Ts, t0 + b * batch_dt, ch0)
         if gains is not None:
             g = np.asarray(gains, np.float32)
             assert g.shape == (M, A), g.shape
@@ -174,14 +179,14 @@ def quantise_coeffs(w):
 
 
 def fused_beamform_int8(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0, batch_dt=0.0, scale=1.0,
-                        signed=False, gains=None):
+                        signed=False, gains=None, ch0=None):
     """Contract of the fused operator's int8 (requantised) output -- bit-exact:
         W = rne(w * 2^14)  (w: the exact float32 coefficients of fused_tables, i.e. CoeffGenerator's at dt = 0)
         y = sum_k x_k W_k  (exact integers)
         q = clamp(rne(float32(y) * float32(float32(scale) * 2^-14)), -127, 127)
     raw: (B, A, C, T, 2, 2) 8-bit -> int8 (B, 2, C, T/16, 16, 2M)."""
     B, A, C, T, P, Z = raw.shape
-    W = quantise_coeffs(fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt, gains))
+    W = quantise_coeffs(fused_tables(delay_vals, B, C, Ctot, A, xeng_id, Ts, t0, batch_dt, gains, ch0))
     xr = reorder(raw)
     X = (xr.view(np.int8) if signed else xr).astype(np.int64).reshape(B, 2, C, T, 2 * A)
     Y = np.matmul(X, W)

@@ -87,3 +87,42 @@ def test_pipeline_argument_validation_without_gpu():
     with pytest.raises(_lib.BeamformerError, match="null pipeline"):
         _lib.call("bf_pipeline_wait", None, 0, 1)
     assert _lib.load().bf_pipeline_destroy(None) == 0
+
+
+def test_kernel_path_and_contract_flags_are_validated():
+    fake = 1 << 20
+    args = [fake, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0]
+    with pytest.raises(_lib.BeamformerError, match="unknown kernel path"):
+        _lib.call("bf_beamform_fused", *args, 0x600, 1.0, None)
+    with pytest.raises(_lib.BeamformerError, match="unknown workgroup order"):
+        _lib.call("bf_beamform_fused", *args, 0x3000, 1.0, None)
+    # Q14 int8 contract: more uint8 antennas than the int32 beam sums hold (A * 255 * 23171 >= 2^31) is refused
+    big = [fake, fake, 1, fake, 1, 4, 16, 364, 1, 1024, 0, 1e-9, 0.0, 0.0]
+    with pytest.raises(_lib.BeamformerError, match="overflows"):
+        _lib.call("bf_beamform_fused", *big, _lib.FUSED_OUT_INT8, 1.0, None)
+
+
+def test_template_int8_overflow_bound():
+    from dpdk_dc_sand_amd.beamforming import FusedBeamformerTemplate
+    FusedBeamformerTemplate(None, 1, 4, 64, 16, 363, 1, out_int8=True)
+    FusedBeamformerTemplate(None, 1, 4, 64, 16, 724, 1, out_int8=True, sample_signed=True)
+    with pytest.raises(ValueError, match="overflow"):
+        FusedBeamformerTemplate(None, 1, 4, 64, 16, 364, 1, out_int8=True)
+    with pytest.raises(ValueError, match="overflow"):
+        FusedBeamformerTemplate(None, 1, 4, 64, 16, 725, 1, out_int8=True, sample_signed=True)
+    FusedBeamformerTemplate(None, 1, 4, 64, 16, 364, 1, out_int8=True, int8_contract="f32")
+    t = FusedBeamformerTemplate(None, 1, 4, 64, 16, 4, 2, out_int8=True, kernel_path="wide", workgroup_order="xcd")
+    assert t.flags == _lib.FUSED_OUT_INT8 | _lib.FUSED_PATH["wide"] | _lib.FUSED_ORDER["xcd"]
+    with pytest.raises(ValueError, match="kernel_path"):
+        FusedBeamformerTemplate(None, 1, 4, 64, 16, 4, 2, kernel_path="fast")
+
+
+def test_product_library_never_reads_the_environment():
+    """Kernel choice and contract switches are explicit flags: the product libbf.so imports no getenv (the
+    measurement knobs live in the BF_DIAG build only)."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    names = {line.split()[-1].split("@")[0] for line in out.stdout.splitlines() if line.strip()}
+    assert "getenv" not in names and "secure_getenv" not in names

@@ -1,0 +1,189 @@
+"""GPU parity at the benchmarked shapes (BASELINE configs 2-4 at full size), through the C ABI.
+
+The oracle cannot evaluate a whole full-size launch in seconds, so each launch here is the exact shape bench.py
+times, checked three ways:
+* sampled items -- the first and last (batch, channel) items plus random ones, each compared with the oracle run on
+  just that channel slice (`ch0` = the item's absolute channel, `t0` = its batch's steering time).  This catches
+  32-bit offset overflow in the kernels' addressing (the raw cube is exactly 2^31 bytes at configs 2 and 3);
+* a size-independent cross-check over the whole output -- two different kernels (or contracts) on the same input
+  must agree everywhere: int8 Q14 vs requantised-f32 beams within one LSB, and the item vs generic float kernels
+  within the fp32 tolerance;
+* config 4's exact per-GPU shape (256 antennas, 64 beams, T = 256, B = 1, X-engine 7 of 8) against the oracle in
+  full, at a channel count the oracle finishes in seconds (C = 8 and 16, so the XCD slab order engages).
+Reference grid: beamformer/unit_test/test_parameters.py:19 (n_ants up to 256).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from dpdk_dc_sand_amd import accel
+from dpdk_dc_sand_amd.beamforming import FusedBeamformerTemplate
+from tolerance import assert_beams_allclose
+
+pytestmark = pytest.mark.gpu
+
+TS = O.TS_MEERKAT
+CONFIGS = {  # bench.py WORKLOADS (A, M, C, T, B, Ctot, xeng_id)
+    "cfg2": (64, 1, 4096, 256, 8, 4096, 0),
+    "cfg3": (64, 16, 4096, 256, 8, 4096, 0),
+    "cfg4": (256, 64, 4096, 256, 1, 32768, 7),
+}
+
+
+def delay_model(M, A, seed):
+    rng = np.random.default_rng(seed)
+    d = np.zeros((1, M, A, 4), np.float32)
+    d[..., 0] = rng.uniform(0, 10 * TS, (M, A))
+    d[..., 1] = rng.uniform(-1e-9, 1e-9, (M, A))
+    d[..., 2] = rng.uniform(-np.pi, np.pi, (M, A))
+    d[..., 3] = rng.uniform(-1, 1, (M, A))
+    return d
+
+
+def random_bytes(shape, seed, signed):
+    n = int(np.prod(shape))
+    buf = np.frombuffer(np.random.default_rng(seed).bytes(n), np.int8 if signed else np.uint8)
+    return buf.reshape(shape)
+
+
+def sample_items(B, C, n, seed):
+    rng = np.random.default_rng(seed)
+    items = {(0, 0), (B - 1, C - 1), (B - 1, 0), (0, C - 1)}
+    while len(items) < n:
+        items.add((int(rng.integers(B)), int(rng.integers(C))))
+    return sorted(items)
+
+
+T0 = 1e-3
+
+
+def batch_dt(cfg):
+    A, M, C, T, B, Ctot, xeng = CONFIGS[cfg]
+    return T * 2 * Ctot * TS
+
+
+def launch(context, queue, cfg, raw, d, signed, **kw):
+    """One full-size fused launch (input resident on the device); returns the beams on the host."""
+    A, M, C, T, B, Ctot, xeng = CONFIGS[cfg]
+    op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, sample_period=TS, delay_channels=1,
+                                 sample_signed=signed, t0=T0, batch_dt=batch_dt(cfg), **kw).instantiate(queue)
+    op.ensure_all_bound()
+    op.buffer("inSamples").set(queue, raw)
+    op.buffer("delay_vals").set(queue, d)
+    op()
+    return op.buffer("outData").get(queue)
+
+
+def item_oracle(cfg, raw, d, b, c, signed, int8=False, scale=None):
+    """The oracle on one (batch, channel) item of a full-size launch: the channel slice at its absolute channel
+    and its batch's steering time.  Returns (beams (2, T/16, 16, 2M), the slice, the item's coefficient table)."""
+    A, M, C, T, B, Ctot, xeng = CONFIGS[cfg]
+    kw = dict(xeng_id=xeng, t0=T0 + b * batch_dt(cfg), batch_dt=batch_dt(cfg), ch0=C * xeng + c)
+    sl = np.ascontiguousarray(raw[b:b + 1, :, c:c + 1])
+    if int8:
+        return O.fused_beamform_int8(sl, d, Ctot, scale=scale, signed=signed, **kw)[0, :, 0], sl, None
+    w = O.fused_tables(d, 1, 1, Ctot, A, **kw)
+    return O.fused_beamform(sl, d, Ctot, signed=signed, **kw)[0, :, 0], sl, w
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4"])
+@pytest.mark.parametrize("signed", [True, False])
+def test_full_size_int8_sampled_and_cross_contract(context, command_queue, cfg, signed):
+    """int8 beams at the benched shape: sampled items bit-exact to the integer contract; over the whole output the
+    Q14 beams and the requantised-f32 beams differ by at most one LSB, in under 1 % of the values."""
+    A, M, C, T, B, Ctot, xeng = CONFIGS[cfg]
+    raw = random_bytes((B, A, C, T, 2, 2), seed=11 + A + M, signed=signed)
+    d = delay_model(M, A, seed=5 + M)
+    scale = 1 / 64
+    q14 = launch(context, command_queue, cfg, raw, d, signed, out_int8=True, out_scale=scale)
+    for b, c in sample_items(B, C, 12, seed=A + M):
+        ref, _, _ = item_oracle(cfg, raw, d, b, c, signed, int8=True, scale=scale)
+        np.testing.assert_array_equal(q14[b, :, c], ref, err_msg=f"{cfg} item (b={b}, c={c})")
+    qf = launch(context, command_queue, cfg, raw, d, signed, out_int8=True, out_scale=scale, int8_contract="f32")
+    diff = np.abs(q14.astype(np.int16) - qf.astype(np.int16))
+    assert int(diff.max()) <= 1, f"{cfg}: Q14 and requantised-f32 int8 beams differ by {int(diff.max())} LSB"
+    rate = float(np.count_nonzero(diff)) / diff.size
+    print(f"{cfg} signed={signed}: Q14 vs requantise(f32) mismatch rate {rate:.3e} over {diff.size} values")
+    assert rate < 0.01
+    assert np.abs(q14.astype(int)).max() >= 8  # not a trivially zero case
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4"])
+def test_full_size_f32_sampled_and_cross_kernel(context, command_queue, cfg):
+    """float32 beams at the benched shape: sampled items within the fp32 tolerance of the oracle; the automatic
+    kernel and the generic kernel (different addressing code) agree over the whole output within the tolerance."""
+    A, M, C, T, B, Ctot, xeng = CONFIGS[cfg]
+    signed = True
+    raw = random_bytes((B, A, C, T, 2, 2), seed=3 + A + M, signed=signed)
+    d = delay_model(M, A, seed=9 + M)
+    y = launch(context, command_queue, cfg, raw, d, signed)
+    for b, c in sample_items(B, C, 8, seed=2 * A + M):
+        ref, sl, w = item_oracle(cfg, raw, d, b, c, signed)
+        assert_beams_allclose(y[b:b + 1, :, c:c + 1], ref[None, :, None], O.reorder(sl), w, signed=signed)
+    yg = launch(context, command_queue, cfg, raw, d, signed, kernel_path="generic")
+    # two float32 evaluations of the same sums: |diff| <= 2^-19 * sum_k |x_k w_k| <= 2^-19 * 128 * 2A (|w| <= 1)
+    bound = 2.0 ** -19 * 128 * 2 * A
+    worst = float(np.max(np.abs(y - yg)))
+    assert worst <= bound, f"{cfg}: auto and generic float kernels differ by {worst} > {bound}"
+
+
+@pytest.mark.parametrize("C", [8, 16])
+@pytest.mark.parametrize("signed", [True, False])
+def test_cfg4_shape_matches_oracle(context, command_queue, C, signed):
+    """Config 4's per-GPU item shape (A = 256, M = 64, T = 256, B = 1, Ctot = 32768, X-engine 7): every wave of the
+    4-wave wide kernels carries valid samples (T = 256), XCD slab order (C % 8 == 0).  int8 bit-exact, f32 within
+    the tolerance, over the whole output."""
+    A, M, T, B, Ctot, xeng = 256, 64, 256, 1, 32768, 7
+    raw = random_bytes((B, A, C, T, 2, 2), seed=C + int(signed), signed=signed)
+    d = delay_model(M, A, seed=C)
+    t0, bdt = 2e-3, T * 2 * Ctot * TS
+    common = dict(xeng_id=xeng, sample_period=TS, delay_channels=1, sample_signed=signed, t0=t0, batch_dt=bdt)
+    q8 = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, out_int8=True, out_scale=1 / 128,
+                                 **common).instantiate(command_queue)
+    q8.ensure_all_bound()
+    q8.buffer("inSamples").set(command_queue, raw)
+    q8.buffer("delay_vals").set(command_queue, d)
+    q8()
+    q = q8.buffer("outData").get(command_queue)
+    ref = O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, scale=1 / 128, signed=signed)
+    np.testing.assert_array_equal(q, ref)
+    assert np.abs(ref.astype(int)).max() >= 8
+    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, **common).instantiate(command_queue)
+    fu.ensure_all_bound()
+    fu.buffer("inSamples").set(command_queue, raw)
+    fu.buffer("delay_vals").set(command_queue, d)
+    fu()
+    y = fu.buffer("outData").get(command_queue)
+    assert_beams_allclose(y, O.fused_beamform(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, signed=signed),
+                          O.reorder(raw), O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, t0=t0, batch_dt=bdt),
+                          signed=signed)
+
+
+def test_int8_overflow_bound_is_enforced(context, command_queue):
+    """The Q14 path sums in int32: at unit gain |y| <= A * 255 * 23171 (uint8), so A = 363 is the largest uint8
+    antenna count.  All-255 samples at zero phase hit the largest real part exactly; one antenna more is refused."""
+    B, C, T, M, Ctot = 1, 1, 16, 1, 8
+    d = np.zeros((1, M, 363, 4), np.float32)
+    raw = np.full((B, 363, C, T, 2, 2), 255, np.uint8)
+    op = FusedBeamformerTemplate(context, B, C, Ctot, T, 363, M, delay_channels=1, out_int8=True,
+                                 out_scale=2.0 ** -10).instantiate(command_queue)
+    op.ensure_all_bound()
+    op.buffer("inSamples").set(command_queue, raw)
+    op.buffer("delay_vals").set(command_queue, d)
+    op()
+    q = op.buffer("outData").get(command_queue)
+    ref = O.fused_beamform_int8(raw, d, Ctot, scale=2.0 ** -10)
+    assert int(ref[0, 0, 0, 0, 0, 0]) == 90  # rne(363 * 255 * 2^14 * 2^-24)
+    np.testing.assert_array_equal(q, ref)
+    with pytest.raises(ValueError, match="overflow"):
+        FusedBeamformerTemplate(context, B, C, Ctot, T, 364, M, delay_channels=1, out_int8=True)
+    # the C ABI refuses it too (no gains given)
+    from dpdk_dc_sand_amd import _lib
+    x = accel.DeviceArray(context, (B, 364, C, T, 2, 2), np.uint8)
+    dv = accel.DeviceArray(context, (1, M, 364, 4), np.float32)
+    y = accel.DeviceArray(context, (B, 2, C, T // 16, 16, 2 * M), np.int8)
+    with pytest.raises(_lib.BeamformerError, match="overflows"):
+        _lib.call("bf_beamform_fused", x.ptr, dv.ptr, 1, y.ptr, B, C, T, 364, M, Ctot, 0, TS, 0.0, 0.0,
+                  _lib.FUSED_OUT_INT8, 1.0, command_queue.handle)
+    # float beams and the requantised-f32 int8 contract have no such bound
+    FusedBeamformerTemplate(context, B, C, Ctot, T, 364, M, delay_channels=1, out_int8=True, int8_contract="f32")

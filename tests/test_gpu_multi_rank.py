@@ -1,0 +1,120 @@
+"""Multi-rank channel sharding on the GPU through libbf, on the one visible MI355X.
+
+Two fresh child processes (ranks of a gloo world of 2) share the GPU.  Rank 0 holds a full-band raw cube; the
+channel scatter (dpdk_dc_sand_amd.shard) gives each rank its X-engine's contiguous channel slice; each rank beamforms
+its slice with `FusedBeamformerTemplate(..., xeng_id=rank)` -- the reference's absolute-channel convention
+`ichannel = c + C * xeng_id` (coeff_generator.py:49-53) -- and the beams are gathered back.  The gathered band must
+equal the full-band oracle: int8 bit-exact, float32 within the stated tolerance.
+
+`test_bench_multi_rank_rehearsal` runs bench.py itself under torch.distributed.run with two ranks on this GPU and
+the gloo scatter backend (RCCL cannot put two ranks on one device); the driver's 8-GPU run uses the nccl backend.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, out_dir):
+    import torch.distributed as dist  # torch before libbf: one HIP runtime
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O
+    from dpdk_dc_sand_amd import accel
+    from dpdk_dc_sand_amd.beamforming import FusedBeamformerTemplate
+    from dpdk_dc_sand_amd.shard import gather_channel_slices, scatter_channel_slices
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B, A, M, T, C = 2, 64, 16, 256, 8
+        Ctot = C * world
+        ts = O.TS_MEERKAT
+        bdt = T * 2 * Ctot * ts
+        rng = np.random.default_rng(5)
+        d = np.zeros((1, M, A, 4), np.float32)
+        d[..., 0] = rng.uniform(0, 10 * ts, (M, A))
+        d[..., 1] = rng.uniform(-1e-9, 1e-9, (M, A))
+        d[..., 2] = rng.uniform(-np.pi, np.pi, (M, A))
+        d[..., 3] = rng.uniform(-1, 1, (M, A))
+        raw = rng.integers(-128, 128, (B, A, Ctot, T, 2, 2), dtype=np.int8) if rank == 0 else None
+        mine = scatter_channel_slices(raw, (B, A, C, T, 2, 2), np.int8, rank, world)
+
+        ctx = accel.create_some_context(device=0)
+        queue = ctx.create_command_queue()
+        out = {}
+        for name, kw in (("int8", dict(out_int8=True, out_scale=1 / 64)), ("f32", {})):
+            op = FusedBeamformerTemplate(ctx, B, C, Ctot, T, A, M, xeng_id=rank, sample_period=ts, delay_channels=1,
+                                         sample_signed=True, t0=1e-3, batch_dt=bdt, **kw).instantiate(queue)
+            op.ensure_all_bound()
+            op.buffer("inSamples").set(queue, mine)
+            op.buffer("delay_vals").set(queue, d)
+            op()
+            out[name] = gather_channel_slices(op.buffer("outData").get(queue), rank, world)
+        if rank == 0:
+            q_ref = O.fused_beamform_int8(raw, d, Ctot, t0=1e-3, batch_dt=bdt, scale=1 / 64, signed=True)
+            y_ref = O.fused_beamform(raw, d, Ctot, t0=1e-3, batch_dt=bdt, signed=True)
+            w = O.fused_tables(d, B, Ctot, Ctot, A, t0=1e-3, batch_dt=bdt)
+            np.savez(os.path.join(out_dir, "result.npz"), q=out["int8"], q_ref=q_ref, y=out["f32"], y_ref=y_ref,
+                     x=O.reorder(raw), w=w)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_channel_sharded_hip_beamforming_matches_full_band(tmp_path):
+    world = 2
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "tests")]))
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import test_gpu_multi_rank as t; "
+            "t._rank_main(int(sys.argv[1]), %d, %d, %r)") % (ROOT, os.path.join(ROOT, "tests"), world, port,
+                                                               str(tmp_path))
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], env=env, cwd=ROOT) for r in range(world)]
+    try:
+        rcs = [p.wait(timeout=110) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0] * world, rcs
+    from tolerance import assert_beams_allclose
+    r = np.load(tmp_path / "result.npz")
+    np.testing.assert_array_equal(r["q"], r["q_ref"])
+    assert np.abs(r["q_ref"].astype(int)).max() >= 8
+    assert_beams_allclose(r["y"], r["y_ref"], r["x"], r["w"], signed=True)
+
+
+def test_bench_multi_rank_rehearsal(tmp_path):
+    """bench.py --gpus 2 under torch.distributed.run: both ranks time their own channel shard (X-engines 0 and 1),
+    the input arrives through the scatter (gloo backend here), and rank 0 prints one JSON line with the whole-job
+    value and the scatter report."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
+           "--warmup", "1", "--settle-ms", "0", "--scatter-backend", "gloo", "--workload", "cfg2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["scatter"]["backend"] == "gloo" and line["scatter"]["ranks"] == 2
+    assert line["scatter"]["bytes_per_rank"] == 8 * 64 * 4096 * 256 * 4
+    assert line["value"] > 0

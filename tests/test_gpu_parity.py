@@ -156,6 +156,8 @@ def test_matrix_multiply_golden(context, command_queue, case):
     x = voltages(case, (B, 2, C, T // 16, 16, A, 2))
     op = MatrixMultiplyTemplate(context, A, C, T, M, B).instantiate(command_queue)
     (y,) = run(op, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
+    # the reference's own bar on the reference's own (uniform-delay) inputs: beamform_mult_kernel_test.py:267-269
+    np.testing.assert_allclose(y, get(case, "output"), rtol=1e-4, atol=1e-4)
     assert_beams_allclose(y, get(case, "output"), x, w)
 
 
@@ -175,7 +177,9 @@ def test_beamform(context, command_queue, n_batches, n_ants, n_channels, n_sampl
         command_queue)
     (y,) = run(mm, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
     w_ref = O.coeffs(d, n_batches, 2, C, n_channels, n_ants, n_beams, xeng_id)
-    assert_beams_allclose(y, O.complex_mult(x, w_ref), x, w_ref)
+    expected = O.complex_mult(x, w_ref)
+    np.testing.assert_allclose(y, expected, rtol=1e-4, atol=1e-4)  # beamform_mult_kernel_test.py:267-269
+    assert_beams_allclose(y, expected, x, w_ref)
 
 
 @pytest.mark.parametrize("A,M,C,T,signed", [
@@ -210,6 +214,7 @@ def test_op_sequence_golden(context, command_queue):
     op()
     y = op.beamform_mult.buffer("outData").get(command_queue)
     d = get("opseq_cfg1", "delays")
+    np.testing.assert_allclose(y, get("opseq_cfg1", "output"), rtol=1e-4, atol=1e-4)  # beamform_op_sequence_test.py:198-199
     assert_beams_allclose(y, get("opseq_cfg1", "output"), O.reorder(raw), O.coeffs(d, B, 2, C, Ctot, A, M, 0))
 
 
@@ -246,24 +251,19 @@ def test_fused_equals_op_sequence_bitwise(context, command_queue, fused_path):
     seq()
     y_seq = seq.beamform_mult.buffer("outData").get(command_queue)
     fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=2, sample_period=TS,
-                                 exact_coeffs=True).instantiate(command_queue)
+                                 exact_coeffs=True, kernel_path=fused_path).instantiate(command_queue)
     (y_fu,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     np.testing.assert_array_equal(y_fu, y_seq)
     assert_beams_allclose(y_fu, O.op_sequence(raw, d, C, Ctot, A, M, xeng_id=2), O.reorder(raw),
                           O.coeffs(d, B, 2, C, Ctot, A, M, 2))
 
 
-@pytest.fixture(params=["item", "pipe", "generic", "wide", "wide32"])
-def fused_path(request, monkeypatch):
-    """Run a fused test through each kernel: the single-item kernel (default for A <= 64, T <= 256), the
-    persistent pipelined kernel, the generic kernel, and the wide kernel (default for many antennas x beams;
-    64- and 32-beam slabs).  int8 output has its own kernels and ignores 'wide'."""
-    if request.param == "wide32":
-        monkeypatch.setenv("BF_FUSED_WIDE_TW", "1")
-        monkeypatch.setenv("BF_FUSED_KERNEL", "wide")
-        return "wide"
-    monkeypatch.delenv("BF_FUSED_GENERIC", raising=False)
-    monkeypatch.setenv("BF_FUSED_KERNEL", request.param)
+@pytest.fixture(params=["auto", "item", "pipe", "generic", "wide", "wide16"])
+def fused_path(request):
+    """Run a fused test through each kernel (FusedBeamformerTemplate kernel_path = BF_FUSED_PATH_* flags): the
+    automatic choice, the single-item kernel (A <= 64, T <= 256), the persistent pipelined kernel, the generic
+    kernel, and the wide kernel (many antennas x beams) with 32- and 16-beam slabs.  A path that does not fit a shape
+    falls through to one that does."""
     return request.param
 
 
@@ -282,8 +282,8 @@ def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C
         raw = raw.view(np.int8)
     t0, bdt = 2.5e-3, 256 * 8192 * TS
     fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, sample_period=TS, delay_channels=dch,
-                                 sample_signed=signed, t0=t0, batch_dt=bdt, exact_coeffs=exact).instantiate(
-                                     command_queue)
+                                 sample_signed=signed, t0=t0, batch_dt=bdt, exact_coeffs=exact,
+                                 kernel_path=fused_path).instantiate(command_queue)
     (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     ref = O.fused_beamform(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, signed=signed)
     w = O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, t0=t0, batch_dt=bdt)
@@ -296,11 +296,10 @@ def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C
     (4, 1, 16, 1024, 1, 16, True), (80, 24, 3, 16, 3, 1, True), (32, 8, 4, 64, 2, 1, False),
     (48, 12, 2, 128, 2, 1, False), (33, 5, 3, 80, 2, 3, True), (16, 8, 3, 48, 2, 1, True),
     (64, 16, 2, 112, 1, 1, False), (40, 32, 2, 64, 1, 2, True)])
-@pytest.mark.parametrize("i8_kernel", ["item", "generic", "wide"])
-def test_fused_int8_bit_exact(context, command_queue, monkeypatch, i8_kernel, A, M, C, T, B, dch, signed):
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide"])
+def test_fused_int8_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """int8 (requantised) beams: the integer MFMA path reproduces the oracle's integer contract bit for bit, on the
     item kernel (A <= 64, T <= 256; others fall through to generic) and the generic kernel (any A, T)."""
-    monkeypatch.setenv("BF_FUSED_KERNEL", i8_kernel)
     Ctot, xeng, t0, bdt = 4096, 1, 1e-3, 256 * 8192 * TS
     d = random_delays(dch, M, A, A * 7 + M)
     rng = np.random.default_rng(A * 3 + C)
@@ -309,7 +308,8 @@ def test_fused_int8_bit_exact(context, command_queue, monkeypatch, i8_kernel, A,
         raw = raw.view(np.int8)
     for scale in (1.0 / 64, 1.0 / 16):
         op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=dch, sample_signed=signed,
-                                     out_int8=True, out_scale=scale, t0=t0, batch_dt=bdt).instantiate(command_queue)
+                                     out_int8=True, out_scale=scale, t0=t0, batch_dt=bdt,
+                                     kernel_path=i8_kernel).instantiate(command_queue)
         (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
         ref = O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, scale=scale, signed=signed)
         assert q.dtype == np.int8
@@ -344,29 +344,28 @@ def test_fused_int8_one_two_beams(context, command_queue, A, T, M, signed):
 
 @pytest.mark.parametrize("order", ["xcd", "channel"])
 @pytest.mark.parametrize("B,C,M", [(2, 16, 16), (3, 24, 8), (1, 8, 16), (2, 40, 12)])
-def test_item_kernels_workgroup_order(context, command_queue, monkeypatch, order, B, C, M):
+def test_item_kernels_workgroup_order(context, command_queue, order, B, C, M):
     """The item kernels' XCD-range workgroup order (C % 8 == 0, >= 8 beams; item_coords) covers every (batch,
     channel) exactly once: int8 bit-exact and f32 within the tolerance, in both orders."""
-    monkeypatch.setenv("BF_ITEM_ORDER", order)
     A, T, Ctot, xeng, bdt = 64, 256, 8 * C, 1, 256 * 8192 * TS
     d = random_delays(1, M, A, B * C + M)
     rng = np.random.default_rng(C * 3 + M)
     raw = rng.integers(-128, 128, (B, A, C, T, 2, 2), dtype=np.int8)
     q8 = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=True,
-                                 out_int8=True, out_scale=1 / 64, batch_dt=bdt).instantiate(command_queue)
+                                 out_int8=True, out_scale=1 / 64, batch_dt=bdt,
+                                 workgroup_order=order).instantiate(command_queue)
     (q,) = run(q8, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     np.testing.assert_array_equal(q, O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, batch_dt=bdt, scale=1 / 64,
                                                            signed=True))
     fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=True,
-                                 batch_dt=bdt).instantiate(command_queue)
+                                 batch_dt=bdt, workgroup_order=order).instantiate(command_queue)
     (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     assert_beams_allclose(y, O.fused_beamform(raw, d, Ctot, xeng_id=xeng, batch_dt=bdt, signed=True), O.reorder(raw),
                           O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, batch_dt=bdt), signed=True)
 
 
-def test_fused_int8_float_path_is_requantised_f32(context, command_queue, monkeypatch):
-    """Measurement path (BF_FUSED_INT8_FLOAT=1): float beams requantised in-kernel == bf_requant(float beams)."""
-    monkeypatch.setenv("BF_FUSED_INT8_FLOAT", "1")
+def test_fused_int8_float_path_is_requantised_f32(context, command_queue):
+    """int8_contract='f32' (BF_FUSED_INT8_VIA_F32): float beams requantised in-kernel == bf_requant(float beams)."""
     B, A, M, C, T, Ctot = 2, 64, 16, 4, 256, 4096
     d = random_delays(1, M, A, 9)
     raw = O.u8_voltages((B, A, C, T, 2, 2), seed=9).view(np.int8)
@@ -375,7 +374,7 @@ def test_fused_int8_float_path_is_requantised_f32(context, command_queue, monkey
         command_queue)
     (y,) = run(f32, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     i8 = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, delay_channels=1, sample_signed=True, out_int8=True,
-                                 out_scale=scale).instantiate(command_queue)
+                                 out_scale=scale, int8_contract="f32").instantiate(command_queue)
     (q,) = run(i8, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     np.testing.assert_array_equal(q, O.requantise(y, scale))
     rq = RequantTemplate(context, y.shape, scale).instantiate(command_queue)
@@ -409,7 +408,8 @@ def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, 
     if signed:
         raw = raw.view(np.int8)
     fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=dch, sample_signed=signed,
-                                 t0=t0, batch_dt=bdt, exact_coeffs=exact, beam_weights=True).instantiate(command_queue)
+                                 t0=t0, batch_dt=bdt, exact_coeffs=exact, beam_weights=True,
+                                 kernel_path=fused_path).instantiate(command_queue)
     g = rng.uniform(-1.5, 1.5, (M, A)).astype(np.float32)
     g[0, : A // 2] = 0.0  # switched-off inputs
     for m in range(M):
@@ -430,10 +430,9 @@ def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, 
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
     (64, 16, 3, 256, 2, 1, True), (64, 16, 2, 256, 2, 1, False), (19, 3, 4, 48, 2, 4, False),
     (130, 9, 2, 64, 1, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["item", "generic", "wide"])
-def test_fused_int8_beam_weights_bit_exact(context, command_queue, monkeypatch, i8_kernel, A, M, C, T, B, dch, signed):
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide"])
+def test_fused_int8_beam_weights_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """Weighted int8 beams: Q14 limbs of the weighted float32 coefficients, bit-exact to the integer contract."""
-    monkeypatch.setenv("BF_FUSED_KERNEL", i8_kernel)
     Ctot, xeng, t0, bdt = 4096, 2, 1e-3, 256 * 8192 * TS
     d = random_delays(dch, M, A, A * 3 + M)
     rng = np.random.default_rng(A * 11 + C)
@@ -443,7 +442,7 @@ def test_fused_int8_beam_weights_bit_exact(context, command_queue, monkeypatch, 
     g = rng.uniform(-1.9, 1.9, (M, A)).astype(np.float32)
     op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=dch, sample_signed=signed,
                                  out_int8=True, out_scale=1 / 64, t0=t0, batch_dt=bdt,
-                                 beam_weights=True).instantiate(command_queue)
+                                 beam_weights=True, kernel_path=i8_kernel).instantiate(command_queue)
     for m in range(M):
         op.set_beam_weights(m, g[m])
     (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
@@ -470,13 +469,12 @@ def boundary_delays(M, A, seed):
 
 @pytest.mark.parametrize("A,M,C,T,B,signed", [(64, 16, 3, 256, 2, True), (64, 16, 2, 256, 2, False),
                                               (19, 3, 3, 48, 2, False), (256, 64, 1, 32, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["item", "generic", "wide"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide"])
 @pytest.mark.parametrize("weighted", [False, True])
-def test_fused_int8_rounding_boundaries(context, command_queue, monkeypatch, i8_kernel, weighted, A, M, C, T, B,
+def test_fused_int8_rounding_boundaries(context, command_queue, i8_kernel, weighted, A, M, C, T, B,
                                         signed):
     """Q14 coefficients whose exact value sits at a rounding boundary: the fast-phasor + exact-fixup path
     (bf_phase.hpp q14_coeffs) must still reproduce the integer contract bit for bit."""
-    monkeypatch.setenv("BF_FUSED_KERNEL", i8_kernel)
     Ctot, xeng, t0, bdt = 4096, 0, 1e-3, 256 * 8192 * TS
     d = boundary_delays(M, A, A + M)
     rng = np.random.default_rng(A * 5 + M)
@@ -486,7 +484,7 @@ def test_fused_int8_rounding_boundaries(context, command_queue, monkeypatch, i8_
     g = rng.choice(np.float32([1.0, 0.5, -1.0, 0.75]), (M, A)).astype(np.float32) if weighted else None
     op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=signed,
                                  out_int8=True, out_scale=1 / 64, t0=t0, batch_dt=bdt,
-                                 beam_weights=weighted).instantiate(command_queue)
+                                 beam_weights=weighted, kernel_path=i8_kernel).instantiate(command_queue)
     if weighted:
         for m in range(M):
             op.set_beam_weights(m, g[m])
@@ -498,23 +496,22 @@ def test_fused_int8_rounding_boundaries(context, command_queue, monkeypatch, i8_
 
 @pytest.mark.parametrize("A,M,C,T,B", [(1, 1, 1, 16, 1), (2, 1, 3, 16, 2), (16, 24, 2, 16, 1), (32, 33, 1, 32, 1),
                                        (257, 3, 1, 16, 1)])
-@pytest.mark.parametrize("kernel", ["item", "generic", "wide"])
-def test_fused_edge_shapes(context, command_queue, monkeypatch, kernel, A, M, C, T, B):
+@pytest.mark.parametrize("kernel", ["auto", "item", "generic", "wide"])
+def test_fused_edge_shapes(context, command_queue, kernel, A, M, C, T, B):
     """Smallest and ragged shapes on every fused path (paths that do not fit a shape fall through to one that does):
     one antenna / beam / channel / batch, T = 16, M not a multiple of 8, A just past a k-step -- f32 within the
     tolerance and int8 bit-exact."""
-    monkeypatch.setenv("BF_FUSED_KERNEL", kernel)
     Ctot = 8 * C
     d = random_delays(1, M, A, A + M)
     rng = np.random.default_rng(A * M + T)
     raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8)
     fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=1, delay_channels=1,
-                                 batch_dt=1e-4).instantiate(command_queue)
+                                 batch_dt=1e-4, kernel_path=kernel).instantiate(command_queue)
     (y,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     assert_beams_allclose(y, O.fused_beamform(raw, d, Ctot, xeng_id=1, batch_dt=1e-4), O.reorder(raw),
                           O.fused_tables(d, B, C, Ctot, A, xeng_id=1, batch_dt=1e-4))
     q8 = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=1, delay_channels=1, batch_dt=1e-4,
-                                 out_int8=True, out_scale=1 / 8).instantiate(command_queue)
+                                 out_int8=True, out_scale=1 / 8, kernel_path=kernel).instantiate(command_queue)
     (q,) = run(q8, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
     np.testing.assert_array_equal(q, O.fused_beamform_int8(raw, d, Ctot, xeng_id=1, batch_dt=1e-4, scale=1 / 8))
 

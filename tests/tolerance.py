@@ -16,14 +16,20 @@ ATOL = 1e-4
 FP32_DOT = 2.0 ** -20
 
 
+def fp32_tolerance(desired, x_reordered, w, signed=False):
+    """Elementwise bound ATOL + RTOL*|desired| + FP32_DOT * sum_k |x_k w_k| (float64)."""
+    desired = np.asarray(desired, np.float64)
+    mag = O.dot_magnitude(x_reordered, w, signed=signed).reshape(desired.shape)
+    return ATOL + RTOL * np.abs(desired) + FP32_DOT * mag
+
+
 def assert_beams_allclose(actual, desired, x_reordered, w, signed=False):
     """|actual - desired| <= ATOL + RTOL*|desired| + FP32_DOT * sum_k |x_k w_k|, elementwise."""
     actual = np.asarray(actual, np.float64)
     desired = np.asarray(desired, np.float64)
     assert actual.shape == desired.shape, (actual.shape, desired.shape)
-    mag = O.dot_magnitude(x_reordered, w, signed=signed).reshape(desired.shape)
     err = np.abs(actual - desired)
-    tol = ATOL + RTOL * np.abs(desired) + FP32_DOT * mag
+    tol = fp32_tolerance(desired, x_reordered, w, signed)
     bad = err > tol
     if bad.any():
         i = np.unravel_index(np.argmax(err / tol), err.shape)
