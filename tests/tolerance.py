@@ -35,3 +35,35 @@ def assert_beams_allclose(actual, desired, x_reordered, w, signed=False):
         i = np.unravel_index(np.argmax(err / tol), err.shape)
         raise AssertionError(f"{int(bad.sum())}/{err.size} beams outside the fp32 tolerance; worst at {i}: "
                              f"actual {actual[i]!r} desired {desired[i]!r} |err| {err[i]:.3e} tol {tol[i]:.3e}")
+
+
+def assert_reference_bar(actual, desired, x_reordered, w, signed=False, max_fraction=1e-5):
+    """The reference's own assertion, np.testing.assert_allclose(cpu, gpu, rtol=1e-4, atol=1e-4)
+    (beamform_mult_kernel_test.py:267-269, beamform_op_sequence_test.py:198-199), against its float32 CPU result.
+
+    That CPU result is itself rounded at the scale of its partial sums (|partial| ~ 1e3 -> ulp ~ 1e-4), so an output
+    that cancels to near zero can sit 1e-4 from the exact value on the CPU side alone.  Every element that misses the
+    bar must therefore (a) meet the same bar against the exact (float64) product, or (b) be no farther from the exact
+    product than the reference's float32 result is; and such elements must be rare (<= max_fraction).
+    Returns the number of elements that missed the plain bar (reported by the caller)."""
+    a = np.asarray(actual, np.float64)
+    d = np.asarray(desired, np.float64)
+    assert a.shape == d.shape, (a.shape, d.shape)
+    miss = np.abs(a - d) > ATOL + RTOL * np.abs(d)
+    n = int(miss.sum())
+    if not n:
+        return 0
+    assert n <= max(1, max_fraction * a.size), f"{n}/{a.size} beams miss the reference's rtol=atol=1e-4 bar"
+    # exact products of the missing elements only: a = (B, P, C, NB, 16, 2M) <-> x (B, P, C, NB, 16, A, 2), w (B,P,C,2A,2M)
+    B, P, C, NB, S, A, Z = x_reordered.shape
+    X = O._as_real(x_reordered, signed).reshape(B, P, C, NB * S, 2 * A).astype(np.float64)
+    W = np.asarray(w, np.float64)
+    for idx in zip(*np.nonzero(miss.reshape(B, P, C, NB * S, -1))):
+        b, p, c, t, col = (int(v) for v in idx)
+        exact = float(np.dot(X[b, p, c, t], W[b, p, c, :, col]))
+        got = float(a.reshape(B, P, C, NB * S, -1)[b, p, c, t, col])
+        ref = float(d.reshape(B, P, C, NB * S, -1)[b, p, c, t, col])
+        ok = abs(got - exact) <= ATOL + RTOL * abs(exact) or abs(got - exact) <= abs(ref - exact)
+        assert ok, (f"beam {idx}: gpu {got!r}, reference f32 {ref!r}, exact {exact!r}: the GPU misses the bar against "
+                    "the exact product and is farther from it than the reference's own float32 result")
+    return n
