@@ -1177,6 +1177,8 @@ int launch_i8(FusedArgs P, hipStream_t st) {
   const int S8 = (2 * P.A + 63) / 64;
   const int choice = fused_kernel_choice(P);
   const bool small = S8 <= 2 && P.T <= 256;
+  if ((choice == BF_FUSED_PATH_WIDE || (choice == 0 && !small)) && i8_wide_lc_fits(P))
+    return launch_i8_wide_lc<Signed>(P, st);
   if ((choice == BF_FUSED_PATH_WIDE || choice == BF_FUSED_PATH_WIDE16 || (choice == 0 && !small)) && i8_wide_fits(P))
     return launch_i8_wide<Signed>(P, st);
   if (small && choice != BF_FUSED_PATH_GENERIC) {

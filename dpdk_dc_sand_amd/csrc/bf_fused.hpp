@@ -79,10 +79,14 @@ __device__ __forceinline__ void transpose_rows4(uint32_t (&v)[4]) {
 // Kernel-path override of a launch (flags & BF_FUSED_PATH_MASK): 0 automatic, else one of the BF_FUSED_PATH_* values.
 inline int fused_kernel_choice(const FusedArgs& P) { return P.path; }
 
-// Integer wide kernel (bf_wide_i8.hip): int8 beams for many antennas x beams.
+// Integer wide kernels: int8 beams for many antennas x beams.  bf_wide_i8lc.hip (loader/consumer, A in [32, 256],
+// M <= 64: the default) and bf_wide_i8.hip (a workgroup per 16-beam slab: larger shapes, BF_FUSED_PATH_WIDE16).
 bool i8_wide_fits(const FusedArgs& P);
 template <bool Signed>
 int launch_i8_wide(FusedArgs P, hipStream_t st);
+bool i8_wide_lc_fits(const FusedArgs& P);
+template <bool Signed>
+int launch_i8_wide_lc(FusedArgs P, hipStream_t st);
 
 // Wide kernel (bf_wide.hip): returns BF_ERR_ARG without launching when the shape does not fit it.
 bool wide_fits(const FusedArgs& P);

@@ -192,7 +192,10 @@ __device__ __forceinline__ void q14_exact(float4 dv, double ch, double ctot, dou
 // exact-only form (diagnostics / ablation).  Serial = true evaluates the N fast phasors one after another
 // (a scheduling barrier between them): less instruction-level parallelism, but the float64 temporaries of only one
 // phasor are live, which is what lets a kernel whose voltage loads are in flight meanwhile fit more waves.
-template <int N, bool FastFirst = true, bool Serial = false>
+// Branchless = true evaluates every fast phasor (invalid ones on their clamped, finite inputs) and zeroes the
+// invalid results afterwards: no per-coefficient branch, so the N float64 Horner chains interleave (a lone wave per
+// SIMD is otherwise latency-bound on them).
+template <int N, bool FastFirst = true, bool Serial = false, bool Branchless = false>
 __device__ __forceinline__ void q14_coeffs(const float4 (&dv)[N], const float (&g)[N], const bool (&valid)[N],
                                            double ch, double ctot, double ts, double k, double dt, const float* gain,
                                            int (&wc)[N], int (&ws)[N]) {
@@ -202,6 +205,14 @@ __device__ __forceinline__ void q14_coeffs(const float4 (&dv)[N], const float (&
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     wc[j] = ws[j] = 0;
+    if constexpr (Branchless && FastFirst) {
+      int c, s;
+      const bool ok = q14_fast(dv[j], chc, k, dt, uk, g[j] * 16384.0f, &c, &s);
+      wc[j] = valid[j] ? c : 0;
+      ws[j] = valid[j] ? s : 0;
+      flagged |= (valid[j] && !ok) ? 1u << j : 0u;
+      continue;
+    }
     if (!valid[j]) continue;
     if constexpr (FastFirst) {
       if (!q14_fast(dv[j], chc, k, dt, uk, g[j] * 16384.0f, &wc[j], &ws[j])) flagged |= 1u << j;

@@ -37,7 +37,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t w8_rsrc(const uint8_t* base) {
 template <int Mode, bool Buf>
 __device__ __forceinline__ void w8_load(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t rsrc, size_t ant_stride,
                                         uint32_t loff, int s, int A, uint32_t (&d)[8][4]) {
-  const int a0 = w8_step_base(s, A);
+  const int a0 = (Mode & 64) ? 8 * (s & 1) : w8_step_base(s, A);  // 64: diagnostics, 16 antenna rows only
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     if constexpr (Mode & 8) {
@@ -46,7 +46,9 @@ __device__ __forceinline__ void w8_load(const uint8_t* __restrict__ base, __amdg
       continue;
     }
     u32x4_t v;
-    if constexpr (Buf)
+    if constexpr ((Mode & 32) != 0)  // diagnostics: non-temporal loads
+      v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a0 + q) * ant_stride + loff));
+    else if constexpr (Buf)
       v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
                                           rsrc, loff, static_cast<uint32_t>(a0 + q) * static_cast<uint32_t>(ant_stride), 0));
     else
@@ -100,14 +102,20 @@ __device__ __forceinline__ void w8_contract(const int4* __restrict__ fr, int s, 
   }
 }
 
-// Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads.
+// Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads, 16 only the first
+// beam slab of each item works (each item's voltages read once), 32 non-temporal voltage loads.
 template <bool Signed, int Mode = 0, bool Buf = true>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
   int slab, bc;
-  if (P.xcd_order) {  // the slabs of one item back to back on one XCD: later slabs re-read the voltages from L2
+  if constexpr ((Mode & 256) != 0) {  // diagnostics: XCD x streams the contiguous item range [x BC/8, (x+1) BC/8)
+    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
+    slab = local % P.nslabs;
+    bc = x * ((P.B * P.C) >> 3) + local / P.nslabs;
+    if (bc >= P.B * P.C) return;
+  } else if (P.xcd_order) {  // the slabs of one item back to back on one XCD: later slabs re-read from L2
     const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
     slab = local % P.nslabs;
     bc = (local / P.nslabs) * 8 + x;
@@ -116,6 +124,8 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(F
     slab = blockIdx.x % P.nslabs;
     bc = blockIdx.x / P.nslabs;
   }
+  if constexpr ((Mode & 16) != 0)
+    if (slab != 0) return;
   const int b = bc / P.C, c = bc % P.C;
   const int m0 = slab * kW8Beams;
   const int Sp = w8_padded_steps(P.A);
@@ -372,6 +382,19 @@ extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y
     case 4: return bf::launch_w8<true, 4>(P, st);
     case 8: return bf::launch_w8<true, 8>(P, st);
     case 5: return bf::launch_w8<true, 5>(P, st);
+    case 3: return bf::launch_w8<true, 3>(P, st);
+    case 9: return bf::launch_w8<true, 9>(P, st);
+    case 13: return bf::launch_w8<true, 13>(P, st);
+    case 16 + 3: return bf::launch_w8<true, 16 + 3>(P, st);
+    case 32 + 3: return bf::launch_w8<true, 32 + 3>(P, st);
+    case 48 + 3: return bf::launch_w8<true, 48 + 3>(P, st);
+    case 32: return bf::launch_w8<true, 32>(P, st);
+    case 16 + 1: return bf::launch_w8<true, 16 + 1>(P, st);
+    case 64 + 3: return bf::launch_w8<true, 64 + 3>(P, st);
+    case 64 + 16 + 3: return bf::launch_w8<true, 64 + 16 + 3>(P, st);
+    case 256 + 3: return bf::launch_w8<true, 256 + 3>(P, st);
+    case 256 + 16 + 3: return bf::launch_w8<true, 256 + 16 + 3>(P, st);
+    case 256: return bf::launch_w8<true, 256>(P, st);
     case 128: return bf::launch_w8<true, 128>(P, st);  // exact phasors only (no fast attempt)
     default: return BF_ERR_ARG;
   }

@@ -73,7 +73,14 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
                   f"alg {alg / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
 if "w8" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_w8.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
-    w8names = {0: "full (fast+fixup)", 128: "exact-only coef", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 5: "no-coef,no-store"}
+    w8names = {0: "full (fast+fixup)", 128: "exact-only coef", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
+               5: "no-coef,no-store", 3: "no-coef,no-mfma", 9: "no-coef,no-load", 13: "no-coef,no-load,no-st",
+               19: "slab0 only,no-coef,no-mfma", 35: "nt loads,no-coef,no-mfma", 51: "slab0,nt,no-coef,no-mfma",
+               32: "nt loads (full)", 17: "slab0 only,no-coef", 67: "16 ant rows,no-coef,no-mfma",
+               83: "16 rows,slab0,no-coef,no-mfma", 259: "xcd-range,no-coef,no-mfma", 275: "xcd-range,slab0,nc,nm",
+               256: "xcd-range (full)"}
+    if _os.environ.get("W8_MODES"):
+        w8names = {int(m): w8names.get(int(m), str(m)) for m in _os.environ["W8_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
     alg8 = nin + nout // 4 // 4  # int8 beams: 2 B per complex beam sample vs 8
     res = {m: [] for m in w8names}
@@ -94,6 +101,21 @@ if "w8" in _os.environ.get("DIAG_KERNELS", ""):
     for mode in w8names:
         ts = sorted(res[mode])
         print(f"  w8 mode {mode:2d} {w8names[mode]:18s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
+              f"alg {alg8 / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
+if "lc" in _os.environ.get("DIAG_KERNELS", ""):
+    lib.bf_diag_lc.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
+    lcnames = {0: "full", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store", 8: "no-load",
+               9: "no-coef,no-load", 11: "no-coef,no-mfma,no-load", 15: "barriers+lds only"}
+    Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
+    alg8 = nin + nout // 4 // 4
+    res = {m: [] for m in lcnames}
+    for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
+        for mode in lcnames:
+            res[mode].append(timeit(lambda i: lib.bf_diag_lc(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
+                                                             B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
+    for mode in lcnames:
+        ts = sorted(res[mode])
+        print(f"  lc mode {mode:2d} {lcnames[mode]:26s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
               f"alg {alg8 / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
 names_i8 = {0: "full (fast+fixup coef, occ 3)", 128: "exact-only coef", 16: "fast coef (inexact)", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store",
             5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
