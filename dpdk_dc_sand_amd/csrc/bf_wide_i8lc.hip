@@ -2,25 +2,32 @@
 // int8 beams, bit-exact to the integer contract (oracle.fused_beamform_int8).
 //
 // Why a second wide kernel.  The slab-per-workgroup kernel (bf_wide_i8.hip) reads each (batch, channel) item's
-// 256 KiB of voltages once per 16-beam slab (4x, the later reads from L2) and keeps at most two k-steps of loads in
-// flight per wave; its load path alone (no coefficients, no MFMA) took 443 us at config 4 against a 217 us stream
-// ceiling, and it did not get faster when each item was read only once (profiles/r2_*_w8_ablation.txt): it is
-// latency-bound, not traffic-bound.  This kernel reads every voltage byte ONCE per CU and keeps ~96 KiB per CU in
-// flight, continuously, across items:
+// 256 KiB of voltages once per 16-beam slab (4x, the later reads from L2), keeps at most two k-steps of loads in
+// flight per wave and evaluates its phasors between its loads and its MFMAs; its load path alone (no coefficients, no
+// MFMA) took 443 us at config 4 against a 217 us stream ceiling (profiles/r2_w8_ablation*.txt).  Here:
 //
 //   one persistent 512-thread workgroup per CU (LDS-limited), items (b, c) in XCD-contiguous runs;
-//   waves 4..7 are LOADERS: each loads 2 antennas x 16 B per lane per k-step into a 12-deep register ring
-//     (ordinary global loads: a loader wave's vmcnt holds nothing else), builds the MFMA B fragments with one v_perm
-//     per dword (and the x - 128 flip for uint8 samples), and writes them into a 3-slot LDS ring two k-steps ahead
-//     of their use, in the exact lane order the consumers read (ds_read_b128, conflict-free);
-//   waves 0..3 are CONSUMERS: wave w owns beam slab w (16 beams) of every item: it generates its slab's Q14 limb
-//     table (32 KiB at A = 256) for the item in its own LDS region (fast float64 phasors + exact fix-up, no
-//     cross-wave sync), then contracts the item's 4 quarters x 8 k-steps: per k-step 32 v_mfma_i32_16x16x64_i8 on
-//     fragments prefetched one step ahead, requantises and stores each quarter's rows as the slab kernel does.
-//   The ring is handed forward by LDS counters (full / free per slot), not barriers: loaders and consumers run
-//   decoupled, a consumer waits only when its next slot is not yet written.
-// A consumer's vector-memory counter holds only its own delay-model loads and beam stores, so the phasor phase's
-// loads never wait behind the voltage stream (they would: vmcnt completes in order).
+//   waves 4..7 are LOADERS, wave 4 + w pairs with consumer w on one SIMD.  A loader
+//     (1) streams its quarter of every k-step's voltages (2 antennas x 16 B per lane) through a 12-deep register
+//         ring (ordinary global loads: nothing else sits in its vmcnt), builds the MFMA B fragments with one v_perm
+//         per dword (+ the x - 128 flip for uint8) and writes them into a 3-slot LDS ring in consumer lane order;
+//     (2) evaluates beam slab w's Q14 phasors for the NEXT item (fast float64 + exact fix-up) into the other half of
+//         a double-buffered table, in between and while it waits for ring slots;
+//   waves 0..3 are CONSUMERS: wave w contracts slab w of the current item: per k-step 32 v_mfma_i32_16x16x64_i8 on
+//     fragments prefetched one step ahead, then requantises and stores each 64-sample quarter.
+//   So one SIMD co-issues the consumer's MFMAs with its loader's VALU (phasors, perms), which a lone wave cannot.
+//
+// Half table.  A slab's table holds one column per beam, k = (2a, 2a + 1) -> (c, -s): y_re = sum x_re c - x_im s is
+// one MFMA against B1 = (re, im); y_im = sum x_im c + x_re s against B2 = (im, ~re) (bitwise not: -re = ~re + 1 stays
+// in int8 for re = -128), minus sum_a s.  That halves the table (16 KiB per slab at A = 256), which is what lets it be
+// double-buffered beside the ring in 160 KiB of LDS.  uint8 samples run as x - 128: + 128 sum (c - s) for y_re and
+// + 128 sum (c + s) for y_im (column sums kept with the table).
+//
+// Hand-offs are LDS counters that only grow (no s_barrier: waves run decoupled):
+//   full[slot]  loader portions written to a ring slot        free[slot]  consumers done reading it
+//   tready[buf] loader slabs written to a table buffer        tfree[buf]  consumers done with it
+// Relaxed LDS atomics with explicit lgkmcnt waits and compiler-only fences: a workgroup-scope release/acquire would
+// also wait vmcnt(0) and drain a loader's loads in flight.  LDS operations of one wave execute in order.
 #include <algorithm>
 
 #include "bf_fused.hpp"
@@ -32,30 +39,38 @@ namespace {
 constexpr int kLcConsumers = 4;                            // one 16-beam slab each
 constexpr int kLcLoaders = 4;
 constexpr int kLcThreads = 64 * (kLcConsumers + kLcLoaders);
-constexpr int kLcRing = 3;                                 // LDS slots (loaders write two k-steps ahead)
+constexpr int kLcRing = 3;                                 // LDS voltage slots
 constexpr int kLcDepth = 12;                               // register slots in flight per loader (multiple of 3)
 constexpr int kLcSlot = 8 * 1024;                          // (i, pol) fragments of one k-step: 8 x 64 lanes x 16 B
-constexpr int kLcStepTable = 4 * 1024;                     // one k-step of a slab's table: 2 tiles x 2 limbs x 1 KiB
+constexpr int kLcStepTable = 2 * 1024;                     // one k-step of a slab's half table: 2 limbs x 1 KiB
 constexpr int kLcMaxSteps = 8;                             // A <= 256
+constexpr int kLcCorr = 16 * 2 * 4;                        // per slab: 16 beams x (sum c, sum s) int32
 
 __device__ __forceinline__ int lc_step_base(int s, int A) { return min(32 * s, A - 32); }
 
 __device__ __forceinline__ void lc_waitcnt_lgkm0() { __builtin_amdgcn_s_waitcnt(0xc07f); }  // lgkmcnt(0) only
 
-// Ring hand-off by LDS counters (no s_barrier per k-step: waves run decoupled).  full[slot] counts loader portions
-// written, free[slot] counts consumer waves done reading; both only grow.  Relaxed LDS atomics plus explicit
-// lgkmcnt waits and compiler-only fences: a release/acquire at workgroup scope would also wait vmcnt(0) and drain
-// the loaders' loads in flight.  LDS operations of one wave execute in order, so a counter update issued after the
-// data writes (waited for) is seen after them.
-__device__ __forceinline__ void lc_signal(unsigned* ctr) {
-  lc_waitcnt_lgkm0();
+__device__ __forceinline__ void lc_add(unsigned* ctr) {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+// publish: the wave's LDS writes land, then the counter moves
+__device__ __forceinline__ void lc_signal(unsigned* ctr) {
+  lc_waitcnt_lgkm0();
+  lc_add(ctr);
+}
+
+__device__ __forceinline__ bool lc_ready(const unsigned* ctr, unsigned target) {
+  return __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target;
+}
+
+// Every spin is bounded (~0.1 s of sleeps): a hand-off bug then ends the kernel with wrong beams, never a hang.
+constexpr int kLcSpinCap = 1 << 21;
+
 __device__ __forceinline__ void lc_wait(const unsigned* ctr, unsigned target) {
-  while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+  for (int n = 0; !lc_ready(ctr, target) && n < kLcSpinCap; ++n) __builtin_amdgcn_s_sleep(1);
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
@@ -78,28 +93,55 @@ __device__ __forceinline__ LcRun lc_run(int n) {
   return r;
 }
 
-// ---- loader -----------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void lc_item_bc(const FusedArgs& P, const LcRun& run, int k, int* b, int* c) {
+  const int item = run.first + k * run.stride;
+  *b = item / P.C;
+  *c = item - *b * P.C;
+}
+
+struct LcLayout {  // LDS carve-up
+  int8_t* ring;
+  unsigned* ctr;  // full[0..3], free[4..7], tready[8..9], tfree[10..11]
+  int8_t* table0;
+  int tbytes;     // table buffer 1 = table0 + tbytes; the column sums follow both buffers
+  // buffer selects by arithmetic, not by indexing a pointer array (that would live in scratch)
+  __device__ int8_t* table(int buf) const { return table0 + buf * tbytes; }
+  __device__ int* corr(int buf) const {
+    return reinterpret_cast<int*>(table0 + 2 * tbytes) + buf * (kLcConsumers * kLcCorr / 4);
+  }
+};
+
+__device__ __forceinline__ LcLayout lc_layout(int8_t* lds, int S) {
+  LcLayout L;
+  L.ring = lds;
+  L.ctr = reinterpret_cast<unsigned*>(lds + kLcRing * kLcSlot);
+  L.tbytes = kLcConsumers * S * kLcStepTable;
+  L.table0 = lds + kLcRing * kLcSlot + 64;
+  return L;
+}
+
+// ---- loader: voltage ring ------------------------------------------------------------------------------------------
+// Mode (diagnostics only): 1 constant tables (no phasors), 2 no MFMA, 4 no stores, 8 loaders write without loading.
 struct LcLoad {
   uint32_t d[2][4];  // antennas (2 qq, 2 qq + 1) of the loader's group: 4 samples x (p0 re, p0 im, p1 re, p1 im)
 };
 
-// Mode (diagnostics only): 1 constant table (no phasors), 2 no MFMA, 4 no stores, 8 loaders write without loading.
-// The loader's issue cursor: the next k-step to load (wave-uniform, advanced one step per issue; clamped to the last
-// step: the loads past the end are unconditional re-loads that are never written).
+// The issue cursor: the next k-step to load (wave-uniform, one step per issue; clamped to the last step: the loads
+// past the end are unconditional re-loads that are never written).
 struct LcCursor {
-  int t, s, q, k;       // global step, step in quarter, quarter, item in the run
-  const uint8_t* item;  // the item's base: raw + ((b A + 0) C + c) T 4
+  int t, s, q, k;
+  const uint8_t* item;  // raw + (b A C + c) T 4
 };
 
 __device__ __forceinline__ const uint8_t* lc_item_base(const FusedArgs& P, const LcRun& run, int k) {
-  const int item = run.first + k * run.stride;
-  const int b = item / P.C, c = item - b * P.C;
+  int b, c;
+  lc_item_bc(P, run, k, &b, &c);
   return P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
 }
 
 __device__ __forceinline__ void lc_advance(const FusedArgs& P, const LcRun& run, int S, int NQ, int nsteps,
                                            LcCursor& u) {
-  if (u.t + 1 >= nsteps) return;  // stay on the last step
+  if (u.t + 1 >= nsteps) return;
   ++u.t;
   if (++u.s == S) {
     u.s = 0;
@@ -111,7 +153,7 @@ __device__ __forceinline__ void lc_advance(const FusedArgs& P, const LcRun& run,
   }
 }
 
-template <int Mode = 0>
+template <int Mode>
 __device__ __forceinline__ void lc_issue(const FusedArgs& P, const LcCursor& u, int w, int tl, int qq, LcLoad& L) {
   if constexpr ((Mode & 8) != 0) {
 #pragma unroll
@@ -132,7 +174,7 @@ __device__ __forceinline__ void lc_issue(const FusedArgs& P, const LcCursor& u, 
   }
 }
 
-// B fragment dword qq of consumer lane (tl, w) for every (sample i, pol p): antennas (2 qq, 2 qq + 1) of group w.
+// B1 fragment dword qq of consumer lane (tl, w) for every (sample i, pol p): antennas (2 qq, 2 qq + 1) of group w.
 template <bool Signed>
 __device__ __forceinline__ void lc_write(int8_t* slot, int w, int tl, int qq, const LcLoad& L) {
   uint32_t* base = reinterpret_cast<uint32_t*>(slot + (tl + 16 * w) * 16 + 4 * qq);
@@ -141,97 +183,107 @@ __device__ __forceinline__ void lc_write(int8_t* slot, int w, int tl, int qq, co
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       uint32_t v = __builtin_amdgcn_perm(L.d[1][i], L.d[0][i], p ? kSelP1 : kSelP0);
-      if constexpr (!Signed) v ^= 0x80808080u;  // x - 128 as int8 (128 * column sum added back by the consumer)
+      if constexpr (!Signed) v ^= 0x80808080u;  // x - 128 as int8
       base[(i * 2 + p) * 256] = v;              // fragment (i, p) block is 1 KiB = 256 dwords
     }
 }
 
-template <bool Signed, int Mode = 0>
-__device__ __forceinline__ void lc_loader(const FusedArgs& P, const LcRun& run, int S, int NQ, int nsteps, int8_t* ring,
-                                          unsigned* full, unsigned* free_, int nact, int w, int lane) {
-  const int tl = lane & 15, qq = lane >> 4;
-  LcLoad R[kLcDepth];
-  LcCursor u{0, 0, 0, 0, lc_item_base(P, run, 0)};
+// ---- loader: phasor table of one slab -----------------------------------------------------------------------------
+// Lane (m' = lane & 15, h = lane >> 4) owns the A-fragment entry of beam 16 w + m', antennas 8 h .. 8 h + 7 of every
+// k-step s: 16 bytes per limb = 8 x (c, -s).  Work unit e = (s, half): 4 antennas 8 h + 4 half + j, the delay model
+// of unit e + 1 in flight meanwhile.
+struct LcTable {
+  int e, E;          // next unit, units per item (2 S)
+  int k;             // item being tabled
+  int cs[4], ss[4];  // first half of the current step (Q14)
+  int sumc, sums;    // the lane's partial column sums
+  float4 dvn[4];
+  float gn[4];
+  bool done;
+};
+
+__device__ __forceinline__ void lc_tfetch(const FusedArgs& P, int slab, int c, int e, int lane, float4 (&dv)[4],
+                                          float (&gv)[4]) {
+  const int s = e >> 1, half = e & 1;
+  const int m = min(16 * slab + (lane & 15), P.M - 1);
+  const int cd = P.delay_channels == 1 ? 0 : c;
+  const float4* dv_row = P.dv + (static_cast<size_t>(cd) * P.M + m) * P.A;
+  const float* gsrc = P.gain ? P.gain : reinterpret_cast<const float*>(P.dv);  // unconditional load, ignored
 #pragma unroll
-  for (int d = 0; d < kLcDepth; ++d) {
-    lc_issue<Mode>(P, u, w, tl, qq, R[d]);
-    lc_advance(P, run, S, NQ, nsteps, u);
-  }
-  for (int t0 = 0; t0 < nsteps; t0 += kLcDepth) {
-#pragma unroll
-    for (int kk = 0; kk < kLcDepth; ++kk) {
-      const int t = t0 + kk;
-      if (t >= nsteps) break;
-      const int slot = kk % kLcRing;  // t0 is a multiple of kLcRing
-      // consumers are done with step t - kLcRing, the slot's previous contents
-      lc_wait(free_ + slot, static_cast<unsigned>(nact * (t / kLcRing)));
-      lc_write<Signed>(ring + slot * kLcSlot, w, tl, qq, R[kk]);
-      lc_issue<Mode>(P, u, w, tl, qq, R[kk]);  // step t + kLcDepth (clamped)
-      lc_advance(P, run, S, NQ, nsteps, u);
-      lc_signal(full + slot);
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int a = min(lc_step_base(s, P.A) + 8 * (lane >> 4) + 4 * half + j, P.A - 1);
+    dv[j] = dv_row[a];
+    gv[j] = gsrc[static_cast<size_t>(m) * P.A + a];
   }
 }
 
-// ---- consumer -----------------------------------------------------------------------------------------------------
-// The slab's Q14 limb table for item (b, c): lane (row = 2 m' + r, h) of tile tt writes its own A-fragment entries
-// (step s: antennas 8 h .. 8 h + 7, column row of the tile).  It evaluates 4 of those 8 phasors and takes the other
-// 4 from lane ^ 1 (same beam, other column).  Column sums (all k) for the uint8 correction come back as corr.
-template <bool Signed>
-__device__ __forceinline__ void lc_table(const FusedArgs& P, int8_t* table, int S, int slab, int b, int c, int lane,
-                                         int (&corr)[2][4]) {
-  const int tl = lane & 15, h = lane >> 4;
-  const int mloc = tl >> 1, r = tl & 1;
-  const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
-  const double ch = static_cast<double>(P.base_ch + c);
-  const int cd = P.delay_channels == 1 ? 0 : c;
-  int colsum[2] = {0, 0};
-  // (tile, step) pairs e = tt S + s, the delay model of pair e + 1 in flight while pair e is evaluated (two register
-  // sets, unrolled by 2: no copies, so the wait before each evaluation is counted, not vmcnt(0)).  The gain load is
-  // unconditional (from the delay table when there are no gains, then ignored) to keep it branch-free.
-  const int E = 2 * S;
-  const float* gsrc = P.gain ? P.gain : reinterpret_cast<const float*>(P.dv);
-  const bool has_gain = P.gain != nullptr;
-  auto fetch = [&](int e, float4 (&dv)[4], float (&gv)[4]) {
-    const int tt = e >= S ? 1 : 0, s = e - tt * S;
-    const int m = min(16 * slab + 8 * tt + mloc, P.M - 1);
-    const float4* dv_row = P.dv + (static_cast<size_t>(cd) * P.M + m) * P.A;
+__device__ __forceinline__ void lc_tstart(const FusedArgs& P, const LcRun& run, int S, int slab, int k, int lane,
+                                          LcTable& T) {
+  T.k = k;
+  T.e = 0;
+  T.E = 2 * S;
+  T.sumc = T.sums = 0;
+  T.done = k >= run.count;
+  if (T.done) return;
+  int b, c;
+  lc_item_bc(P, run, k, &b, &c);
+  lc_tfetch(P, slab, c, 0, lane, T.dvn, T.gn);
+}
+
+// One unit of the table of item T.k into buffer `table`/`corr`; publishes tready after the last unit.
+template <int Mode>
+__device__ __forceinline__ void lc_tunit(const FusedArgs& P, const LcRun& run, int S, int slab, int lane,
+                                         int8_t* table, int* corr, unsigned* tready, LcTable& T) {
+  int b, c;
+  lc_item_bc(P, run, T.k, &b, &c);
+  const int e = T.e, s = e >> 1, half = e & 1;
+  const int h = lane >> 4, mloc = lane & 15, m = 16 * slab + mloc;
+  float4 dv[4];
+  float gv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    dv[j] = T.dvn[j];
+    gv[j] = P.gain ? T.gn[j] : 1.0f;
+  }
+  lc_tfetch(P, slab, c, min(e + 1, T.E - 1), lane, T.dvn, T.gn);  // unconditional (a spare re-load at the end)
+  int wc[4], ws[4];
+  if constexpr ((Mode & 1) != 0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int a = min(lc_step_base(s, P.A) + 8 * h + 4 * r + j, P.A - 1);
-      dv[j] = dv_row[a];
-      gv[j] = gsrc[static_cast<size_t>(m) * P.A + a];
+      wc[j] = 16384 - 7 * j - mloc;
+      ws[j] = 100 * j + h - half;
     }
-  };
-  auto eval = [&](int e, const float4 (&dv)[4], const float (&gv0)[4]) {
-    const int tt = e >= S ? 1 : 0, s = e - tt * S;
-    const int m = 16 * slab + 8 * tt + mloc;
+  } else {
     bool valid[4];
-    float gv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // rows of antennas an earlier step covered stay zero
-      valid[j] = m < P.M && lc_step_base(s, P.A) + 8 * h + 4 * r + j >= 32 * s;
-      gv[j] = has_gain ? gv0[j] : 1.0f;
-    }
-    int wc[4], ws[4];
-    q14_coeffs<4, true, false, true>(dv, gv, valid, ch, P.ctot, P.ts, P.k, dt, P.gain, wc, ws);
-    int pc[4], ps[4];  // partner's 4 phasors (the other half of the 8 antennas)
+    for (int j = 0; j < 4; ++j)  // rows of antennas an earlier step covered stay zero
+      valid[j] = m < P.M && lc_step_base(s, P.A) + 8 * h + 4 * half + j >= 32 * s;
+    const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+    q14_coeffs<4, true, false, true>(dv, gv, valid, static_cast<double>(P.base_ch + c), P.ctot, P.ts, P.k, dt, P.gain,
+                                     wc, ws);
+  }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pc[j] = __shfl_xor(wc[j], 1);
-      ps[j] = __shfl_xor(ws[j], 1);
-    }
-    // antennas 8h + 0..3 are evaluated by r = 0, 8h + 4..7 by r = 1
-    int C8[8], S8[8];
+  for (int j = 0; j < 4; ++j) {
+    T.sumc += wc[j];
+    T.sums += ws[j];
+  }
+  if (half == 0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      C8[j] = r ? pc[j] : wc[j];
-      S8[j] = r ? ps[j] : ws[j];
-      C8[4 + j] = r ? wc[j] : pc[j];
-      S8[4 + j] = r ? ws[j] : ps[j];
+      T.cs[j] = wc[j];
+      T.ss[j] = ws[j];
     }
-    // column r = 0 (the beam's real part): k pair (c, -s); r = 1 (imaginary part): (s, c).  Balanced limbs
-    // W = 256 hi + lo, lo in [-128, 127]: lo byte = W & 255, hi byte = ((W + 128) >> 8) & 255.
+  } else {
+    // 16 bytes per limb: antennas q = 0..7 -> (c, -s).  Balanced limbs W = 256 hi + lo, lo in [-128, 127]:
+    // lo byte = W & 255, hi byte = ((W + 128) >> 8) & 255.
+    int C8[8], N8[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      C8[j] = T.cs[j];
+      N8[j] = -T.ss[j];
+      C8[4 + j] = wc[j];
+      N8[4 + j] = -ws[j];
+    }
     uint32_t hi4[4], lo4[4];
 #pragma unroll
     for (int e2 = 0; e2 < 4; ++e2) {
@@ -239,41 +291,98 @@ __device__ __forceinline__ void lc_table(const FusedArgs& P, int8_t* table, int 
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         const int j = 2 * e2 + f;
-        const int w0 = r ? S8[j] : C8[j];
-        const int w1 = r ? C8[j] : -S8[j];
-        colsum[tt] += w0 + w1;
-        hp[f] = __builtin_amdgcn_perm(static_cast<uint32_t>(w1 + 128), static_cast<uint32_t>(w0 + 128), 0x0c0c0501u);
-        lp[f] = __builtin_amdgcn_perm(static_cast<uint32_t>(w1), static_cast<uint32_t>(w0), 0x0c0c0400u);
+        hp[f] = __builtin_amdgcn_perm(static_cast<uint32_t>(N8[j] + 128), static_cast<uint32_t>(C8[j] + 128),
+                                      0x0c0c0501u);
+        lp[f] = __builtin_amdgcn_perm(static_cast<uint32_t>(N8[j]), static_cast<uint32_t>(C8[j]), 0x0c0c0400u);
       }
       hi4[e2] = __builtin_amdgcn_perm(hp[1], hp[0], 0x05040100u);
       lo4[e2] = __builtin_amdgcn_perm(lp[1], lp[0], 0x05040100u);
     }
-    int8_t* o = table + s * kLcStepTable + (tt * 2) * 1024 + lane * 16;
+    int8_t* o = table + (slab * S + s) * kLcStepTable + lane * 16;
     *reinterpret_cast<u32x4_t*>(o) = u32x4_t{hi4[0], hi4[1], hi4[2], hi4[3]};
     *reinterpret_cast<u32x4_t*>(o + 1024) = u32x4_t{lo4[0], lo4[1], lo4[2], lo4[3]};
-  };
-  float4 dA[4], dB[4];
-  float gA[4], gB[4];
-  fetch(0, dA, gA);
-  for (int e = 0; e < E; e += 2) {  // E = 2 S is even
-    fetch(e + 1, dB, gB);
-    eval(e, dA, gA);
-    fetch(min(e + 2, E - 1), dA, gA);  // unconditional (a spare re-load at the end): no branch, no vmcnt(0)
-    eval(e + 1, dB, gB);
   }
-#pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
-    corr[tt][0] = corr[tt][1] = corr[tt][2] = corr[tt][3] = 0;
-    if constexpr (!Signed) {
-      int v = colsum[tt];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);  // column tl's sum over all k, in every lane (tl, *)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) corr[tt][rr] = 128 * __shfl(v, 4 * h + rr);
+  if (++T.e == T.E) {  // column sums over every antenna of beam m' (lanes m', m' + 16, + 32, + 48)
+    int sc = T.sumc, sn = T.sums;
+    sc += __shfl_xor(sc, 16);
+    sn += __shfl_xor(sn, 16);
+    sc += __shfl_xor(sc, 32);
+    sn += __shfl_xor(sn, 32);
+    if (h == 0) {
+      corr[slab * 32 + 2 * mloc] = sc;
+      corr[slab * 32 + 2 * mloc + 1] = sn;
     }
+    lc_signal(tready);
+    T.done = true;
   }
 }
 
+// Table work for item T.k (buffer T.k & 1) once the consumers have released that buffer (item T.k - 2).
+template <int Mode>
+__device__ __forceinline__ bool lc_try_table(const FusedArgs& P, const LcRun& run, int S, int slab, int lane,
+                                             const LcLayout& L, int nact, LcTable& T) {
+  if (T.done) return false;
+  const int buf = T.k & 1;
+  if (T.e == 0 && !lc_ready(L.ctr + 10 + buf, static_cast<unsigned>(nact * (T.k >> 1)))) return false;
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  lc_tunit<Mode>(P, run, S, slab, lane, L.table(buf), L.corr(buf), L.ctr + 8 + buf, T);
+  return true;
+}
+
+template <bool Signed, int Mode>
+__device__ __forceinline__ void lc_loader(const FusedArgs& P, const LcRun& run, int S, int NQ, int nsteps,
+                                          const LcLayout& L, int nact, int w, int lane) {
+  const int tl = lane & 15, qq = lane >> 4;
+  const int per_item = NQ * S;
+  LcLoad R[kLcDepth];
+  LcCursor u{0, 0, 0, 0, lc_item_base(P, run, 0)};
+#pragma unroll
+  for (int d = 0; d < kLcDepth; ++d) {
+    lc_issue<Mode>(P, u, w, tl, qq, R[d]);
+    lc_advance(P, run, S, NQ, nsteps, u);
+  }
+  // item 0's table up front (its voltages are in flight meanwhile); later items' tables are interleaved with the
+  // ring steps, each as soon as its buffer is released (item k waits for the consumers to finish item k - 2)
+  LcTable T;
+  lc_tstart(P, run, S, w, 0, lane, T);
+  for (int n = 0; !T.done && n < kLcSpinCap; ++n) lc_try_table<Mode>(P, run, S, w, lane, L, nact, T);
+  lc_tstart(P, run, S, w, 1, lane, T);
+  // units tried per ring step before the slot check, so that an item's table keeps pace with the ring
+  const int upt = (2 * S + per_item - 1) / per_item;
+  for (int t0 = 0; t0 < nsteps; t0 += kLcDepth) {
+#pragma unroll
+    for (int kk = 0; kk < kLcDepth; ++kk) {
+      const int t = t0 + kk;
+      if (t >= nsteps) break;
+      const int slot = kk % kLcRing;  // t0 is a multiple of kLcRing
+      // One loop, one table call site (the unrolled ring keeps its register indices static).  Table work never
+      // blocks the ring: a unit whose buffer is not yet released is skipped (the consumers that will release it may
+      // be waiting for this very slot).
+      int budget = upt;
+      for (int n = 0; n < kLcSpinCap; ++n) {
+        if (T.done && T.k + 1 < run.count) lc_tstart(P, run, S, w, T.k + 1, lane, T);
+        const bool did = lc_try_table<Mode>(P, run, S, w, lane, L, nact, T);
+        if (did && --budget > 0) continue;
+        if (lc_ready(L.ctr + 4 + slot, static_cast<unsigned>(nact * (t / kLcRing)))) break;
+        if (!did) __builtin_amdgcn_s_sleep(1);
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      lc_write<Signed>(L.ring + slot * kLcSlot, w, tl, qq, R[kk]);
+      lc_issue<Mode>(P, u, w, tl, qq, R[kk]);  // step t + kLcDepth (clamped)
+      lc_advance(P, run, S, NQ, nsteps, u);
+      lc_signal(L.ctr + slot);
+    }
+  }
+  for (int n = 0; n < kLcSpinCap; ++n) {  // the remaining tables
+    if (T.done) {
+      if (T.k + 1 >= run.count) break;
+      lc_tstart(P, run, S, w, T.k + 1, lane, T);
+    }
+    if (!lc_try_table<Mode>(P, run, S, w, lane, L, nact, T)) __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// ---- consumer ------------------------------------------------------------------------------------------------------
 struct LcFrags {
   i32x4_t f[4][2];  // [sample i][pol]
 };
@@ -288,113 +397,126 @@ __device__ __forceinline__ void lc_read_frags(const int8_t* slot, int lane, LcFr
     }
 }
 
+__device__ __forceinline__ void lc_read_table(const int8_t* step, int lane, i32x4_t& hi, i32x4_t& lo) {
+  const int4 x0 = *reinterpret_cast<const int4*>(step + lane * 16);
+  const int4 x1 = *reinterpret_cast<const int4*>(step + 1024 + lane * 16);
+  hi = i32x4_t{x0.x, x0.y, x0.z, x0.w};
+  lo = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+}
+
+// B2 = (im, ~re) per antenna from B1 = (re, im): bytes [b1, ~b0, b3, ~b2]
+__device__ __forceinline__ i32x4_t lc_b2(const i32x4_t& b1) {
+  i32x4_t r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t v = static_cast<uint32_t>(b1[j]);
+    r[j] = static_cast<int>(__builtin_amdgcn_perm(~v, v, 0x06030401u));
+  }
+  return r;
+}
+
+// Accumulators of one quarter: [pol][sample i][re / im], hi and lo limbs
+struct LcAcc {
+  i32x4_t hi[2][4][2], lo[2][4][2];
+};
+
 template <bool Signed>
 __device__ __forceinline__ void lc_store_quarter(const FusedArgs& P, int b, int c, int q, int m0, int lane,
-                                                 const i32x4_t (&hi)[2][4][2], const i32x4_t (&lo)[2][4][2],
-                                                 const int (&corr)[2][4]) {
+                                                 const LcAcc& acc, const int (&corr)[2][4]) {
   const int tl = lane & 15, h = lane >> 4;
   const int T4 = P.T >> 2, tq = 16 * q + tl, M2 = 2 * P.M;
   const float s32 = P.out_scale * 0x1p-14f;
-  const bool full = m0 + 16 <= P.M && (M2 & 15) == 0;
+  if (tq >= T4) return;
+  const bool full = m0 + 4 * h + 4 <= P.M;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    uint32_t pk[2][4];
+    const size_t prow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int i = 0; i < 4; ++i) {
+      uint32_t qb[2][4];  // [re / im][beam 4 h + r]
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint32_t qb[4];
+      for (int ri = 0; ri < 2; ++ri)
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) qb[rr] = requant_bits((hi[p][i][t][rr] << 8) + lo[p][i][t][rr] + corr[t][rr], s32);
-        pk[t][i] = pack_low_bytes(qb[0], qb[1], qb[2], qb[3]);
-      }
-    const size_t prow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T);
-    if (full) {
+        for (int r = 0; r < 4; ++r)
+          qb[ri][r] = requant_bits((acc.hi[p][i][ri][r] << 8) + acc.lo[p][i][ri][r] + corr[ri][r], s32);
+      // output row bytes 2 m, 2 m + 1 = (re, im) of beam m: beams 4 h .. 4 h + 3 are 8 contiguous bytes
+      const uint32_t w0 = pack_low_bytes(qb[0][0], qb[1][0], qb[0][1], qb[1][1]);
+      const uint32_t w1 = pack_low_bytes(qb[0][2], qb[1][2], qb[0][3], qb[1][3]);
+      int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + i) * M2 + 2 * (m0 + 4 * h);
+      if (full) {
+        *reinterpret_cast<u32x2_t*>(o) = u32x2_t{w0, w1};
+      } else {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) transpose_rows4(pk[t]);  // lane (tl, h): row 4 tq + h, columns 16 t .. 16 t + 15
-      if (tq < T4) {
-        int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 4 * tq + h) * M2 + 2 * m0;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)  // plain stores: L2 merges the four slab waves' 32-B row segments into lines
-          *reinterpret_cast<u32x4_t*>(o + 16 * t) = u32x4_t{pk[t][0], pk[t][1], pk[t][2], pk[t][3]};
-      }
-    } else if (tq < T4) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 4 * tq + i) * M2 + 2 * m0;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int col = 16 * t + 4 * h + rr;
-            if (2 * m0 + col < M2) o[col] = static_cast<int8_t>((pk[t][i] >> (8 * rr)) & 255);
+        for (int r = 0; r < 4; ++r)
+          if (m0 + 4 * h + r < P.M) {
+            const uint32_t wr = r < 2 ? w0 : w1;
+            o[2 * r] = static_cast<int8_t>((wr >> (16 * (r & 1))) & 255);
+            o[2 * r + 1] = static_cast<int8_t>((wr >> (16 * (r & 1) + 8)) & 255);
           }
       }
     }
   }
 }
 
-// A consumer wave: per item its slab's table, then quarters x k-steps.  Step t starts past barrier B_t with slot t's
-// fragments in registers (Fc); it reads its table fragments, prefetches slot t + 1 (written before B_t) into Fn,
-// runs 32 MFMAs on Fc, and ends at B_{t+1}.  Every LDS read is unconditional (the last prefetch reads a stale slot
-// and is never used), so the compiler's lgkmcnt waits stay counted.  The accumulators live only inside a quarter,
-// so the table phase has the register file to itself.
-template <bool Signed, int Mode = 0>
+template <bool Signed, int Mode>
 __device__ __forceinline__ void lc_consumer(const FusedArgs& P, const LcRun& run, int S, int NQ, int nsteps,
-                                            int8_t* ring, unsigned* full, unsigned* free_, int8_t* table, int slab,
-                                            int lane) {
+                                            const LcLayout& L, int slab, int lane) {
+  const int h = lane >> 4;
   LcFrags Fc, Fn;
-  int corr[2][4];
   int t = 0;
-  lc_wait(full, kLcLoaders);  // step 0's slot is written
-  lc_read_frags(ring, lane, Fc);
+  lc_wait(L.ctr, kLcLoaders);  // step 0's slot is written
+  lc_read_frags(L.ring, lane, Fc);
   for (int k = 0; k < run.count; ++k) {
-    const int item = run.first + k * run.stride;
-    const int b = item / P.C, c = item - b * P.C;
-    if constexpr ((Mode & 1) != 0) {
-      if (k == 0)
-        for (int e = 0; e < 2 * S; ++e)
-          *reinterpret_cast<u32x4_t*>(table + e * 2048 + lane * 16) = u32x4_t{0x01020304u, 0x05060708u, 1u, 2u};
-      corr[0][0] = corr[0][1] = corr[0][2] = corr[0][3] = corr[1][0] = corr[1][1] = corr[1][2] = corr[1][3] = 0;
-    } else {
-      lc_table<Signed>(P, table, S, slab, b, c, lane, corr);
+    int b, c;
+    lc_item_bc(P, run, k, &b, &c);
+    const int buf = k & 1;
+    lc_wait(L.ctr + 8 + buf, static_cast<unsigned>(kLcLoaders * ((k >> 1) + 1)));  // every slab of item k is tabled
+    const int8_t* table = L.table(buf) + slab * S * kLcStepTable;
+    int corr[2][4];  // [re / im][beam 4 h + r]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int* cb = L.corr(buf);
+      const int sc = cb[slab * 32 + 2 * (4 * h + r)], sn = cb[slab * 32 + 2 * (4 * h + r) + 1];
+      corr[0][r] = Signed ? 0 : 128 * (sc - sn);
+      corr[1][r] = -sn + (Signed ? 0 : 128 * (sc + sn));
     }
+    i32x4_t ahi, alo;
+    lc_read_table(table, lane, ahi, alo);
     for (int q = 0; q < NQ; ++q) {
-      i32x4_t hi[2][4][2], lo[2][4][2];
+      LcAcc acc;
 #pragma unroll
       for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int tt = 0; tt < 2; ++tt) hi[p][i][tt] = lo[p][i][tt] = i32x4_t{0, 0, 0, 0};
+          for (int ri = 0; ri < 2; ++ri) acc.hi[p][i][ri] = acc.lo[p][i][ri] = i32x4_t{0, 0, 0, 0};
       for (int s = 0; s < S; ++s, ++t) {
-        i32x4_t chi[2], clo[2];
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          const int4 x0 = *reinterpret_cast<const int4*>(table + s * kLcStepTable + (tt * 2) * 1024 + lane * 16);
-          const int4 x1 = *reinterpret_cast<const int4*>(table + s * kLcStepTable + (tt * 2 + 1) * 1024 + lane * 16);
-          chi[tt] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
-          clo[tt] = i32x4_t{x1.x, x1.y, x1.z, x1.w};
-        }
-        lc_signal(free_ + t % kLcRing);  // Fc and the table fragments are in registers: slot t may be refilled
-        const int tn = t + 1 < nsteps ? t + 1 : t;  // the last prefetch re-reads a slot it holds (never used)
-        lc_wait(full + tn % kLcRing, static_cast<unsigned>(kLcLoaders * (tn / kLcRing + 1)));
-        lc_read_frags(ring + (tn % kLcRing) * kLcSlot, lane, Fn);
+        if (t > 0) lc_add(L.ctr + 4 + (t - 1) % kLcRing);  // slot t - 1 was consumed by the last step's MFMAs
+        const int tn = t + 1 < nsteps ? t + 1 : t;          // the last prefetch re-reads a slot it holds (unused)
+        lc_wait(L.ctr + tn % kLcRing, static_cast<unsigned>(kLcLoaders * (tn / kLcRing + 1)));
+        lc_read_frags(L.ring + (tn % kLcRing) * kLcSlot, lane, Fn);
+        i32x4_t nhi = ahi, nlo = alo;
+        if (s + 1 < S) lc_read_table(table + (s + 1) * kLcStepTable, lane, nhi, nlo);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int tt = 0; tt < 2; ++tt) {
-              if constexpr ((Mode & 2) != 0) {
-                hi[p][i][tt] += chi[tt] ^ Fc.f[i][p];
-                lo[p][i][tt] += clo[tt] ^ Fc.f[i][p];
-              } else {
-                hi[p][i][tt] = mfma_i8(chi[tt], Fc.f[i][p], hi[p][i][tt]);
-                lo[p][i][tt] = mfma_i8(clo[tt], Fc.f[i][p], lo[p][i][tt]);
-              }
+          for (int i = 0; i < 4; ++i) {
+            const i32x4_t b2 = lc_b2(Fc.f[i][p]);
+            if constexpr ((Mode & 2) != 0) {
+              acc.hi[p][i][0] += ahi ^ Fc.f[i][p];
+              acc.lo[p][i][0] += alo ^ Fc.f[i][p];
+              acc.hi[p][i][1] += ahi ^ b2;
+              acc.lo[p][i][1] += alo ^ b2;
+            } else {
+              acc.hi[p][i][0] = mfma_i8(ahi, Fc.f[i][p], acc.hi[p][i][0]);
+              acc.lo[p][i][0] = mfma_i8(alo, Fc.f[i][p], acc.lo[p][i][0]);
+              acc.hi[p][i][1] = mfma_i8(ahi, b2, acc.hi[p][i][1]);
+              acc.lo[p][i][1] = mfma_i8(alo, b2, acc.lo[p][i][1]);
             }
+          }
         Fc = Fn;
+        ahi = nhi;
+        alo = nlo;
       }
       if constexpr ((Mode & 4) != 0) {
         int sum = 0;
@@ -403,12 +525,14 @@ __device__ __forceinline__ void lc_consumer(const FusedArgs& P, const LcRun& run
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int tt = 0; tt < 2; ++tt) sum += hi[p][i][tt][0] ^ lo[p][i][tt][3];
+            for (int ri = 0; ri < 2; ++ri) sum += acc.hi[p][i][ri][0] ^ acc.lo[p][i][ri][3];
         if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[lane] = sum;
       } else {
-        lc_store_quarter<Signed>(P, b, c, q, 16 * slab, lane, hi, lo, corr);
+        lc_store_quarter<Signed>(P, b, c, q, 16 * slab, lane, acc, corr);
       }
+      if (q + 1 < NQ) lc_read_table(table, lane, ahi, alo);  // step 0 again for the next quarter
     }
+    lc_signal(L.ctr + 10 + buf);  // the table buffer of item k is free
   }
 }
 
@@ -423,22 +547,19 @@ __global__ __launch_bounds__(kLcThreads, 1) void beamform_fused_i8_wide_lc_kerne
   const int NQ = (P.T + 63) >> 6;
   const int nsteps = run.count * NQ * S;
   const int nact = min(P.nslabs, kLcConsumers);
-  int8_t* ring = reinterpret_cast<int8_t*>(lds_lc);
-  unsigned* full = reinterpret_cast<unsigned*>(ring + kLcRing * kLcSlot);
-  unsigned* free_ = full + 4;
-  int8_t* tables = ring + kLcRing * kLcSlot + 64;
-  if (threadIdx.x < 8) full[threadIdx.x] = 0;  // full[0..3], free[0..3]
-  __syncthreads();                             // the only barrier
+  const LcLayout L = lc_layout(reinterpret_cast<int8_t*>(lds_lc), S);
+  if (threadIdx.x < 16) L.ctr[threadIdx.x] = 0;
+  __syncthreads();  // the only barrier
   if (wave >= kLcConsumers)
-    lc_loader<Signed, Mode>(P, run, S, NQ, nsteps, ring, full, free_, nact, wave - kLcConsumers, lane);
+    lc_loader<Signed, Mode>(P, run, S, NQ, nsteps, L, nact, wave - kLcConsumers, lane);
   else if (wave < nact)
-    lc_consumer<Signed, Mode>(P, run, S, NQ, nsteps, ring, full, free_,
-                              tables + static_cast<size_t>(wave) * S * kLcStepTable, wave, lane);
+    lc_consumer<Signed, Mode>(P, run, S, NQ, nsteps, L, wave, lane);
 }
 
 size_t lc_lds_bytes(const FusedArgs& P) {
   const int S = (P.A + 31) >> 5;
-  return static_cast<size_t>(kLcRing) * kLcSlot + 64 + static_cast<size_t>(kLcConsumers) * S * kLcStepTable;
+  return static_cast<size_t>(kLcRing) * kLcSlot + 64 + 2 * static_cast<size_t>(kLcConsumers) * S * kLcStepTable +
+         2 * kLcConsumers * kLcCorr;
 }
 
 int lc_grid() {
@@ -454,6 +575,9 @@ int lc_grid() {
   return cus;
 }
 
+template <bool Signed, int Mode>
+int launch_lc(FusedArgs P, hipStream_t st);
+
 }  // namespace
 
 bool i8_wide_lc_fits(const FusedArgs& P) {
@@ -461,6 +585,7 @@ bool i8_wide_lc_fits(const FusedArgs& P) {
          static_cast<long long>(P.B) * P.C < (1LL << 31) / (((P.T + 63) >> 6) * ((P.A + 31) >> 5));
 }
 
+namespace {
 template <bool Signed, int Mode>
 int launch_lc(FusedArgs P, hipStream_t st) {
   BF_REQUIRE(i8_wide_lc_fits(P), "bf_beamform_fused: shape does not fit the loader/consumer integer wide kernel");
@@ -469,6 +594,7 @@ int launch_lc(FusedArgs P, hipStream_t st) {
                      dim3(kLcThreads), lc_lds_bytes(P), st, P);
   BF_LAUNCHED("beamform_fused_i8_wide_lc_kernel");
 }
+}  // namespace
 
 template <bool Signed>
 int launch_i8_wide_lc(FusedArgs P, hipStream_t st) {

@@ -1,5 +1,7 @@
 """Host-side logic that needs no GPU: template shapes/attributes mirror the reference, ValueError behaviour,
 accel slot binding and the OpSequence compound-slot aliasing (beamform_op_sequence.py:148-156)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -8,6 +10,7 @@ from dpdk_dc_sand_amd.beamforming import (CoeffGeneratorTemplate, FusedBeamforme
                                           OpSequenceTemplate, PreBeamformReorderTemplate)
 
 TS = 1 / 1712e6
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 class FakeQueue:
@@ -132,3 +135,15 @@ def test_streaming_template():
     assert (t.depth, t.frame_dt, t.input_shape, t.flags) == (3, 2e-3, (2, 4, 8, 32, 2, 2), 2)
     with pytest.raises(ValueError):
         StreamingBeamformerTemplate(None, 2, 8, 64, 32, 4, 3, depth=0)
+
+
+def test_loader_consumer_protocol_has_no_deadlock():
+    """The int8 loader/consumer wide kernel's LDS-counter hand-offs (bf_wide_i8lc.hip), modelled on the CPU and run
+    under random interleavings of 4 loaders and 1-4 consumers: every schedule completes."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("lcsim", os.path.join(ROOT, "tools", "sim", "lc_protocol_sim.py"))
+    sim = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sim)
+    for count, S, NQ, nact in [(16, 8, 4, 4), (3, 1, 1, 1), (7, 2, 1, 2), (9, 3, 2, 3), (2, 1, 1, 4)]:
+        for seed in range(3):
+            assert isinstance(sim.simulate(count, S, NQ, nact, seed=seed), int), (count, S, NQ, nact, seed)
