@@ -75,7 +75,7 @@ PROTOTYPES = {
 # bf_beamform_fused flags (include/bf.h)
 FUSED_SIGNED, FUSED_OUT_INT8, FUSED_EXACT_COEFF, FUSED_INT8_VIA_F32 = 1, 2, 4, 8
 # kernel-path / workgroup-order overrides (tests and measurement; every path computes the same contract)
-FUSED_PATH = {"auto": 0, "item": 0x100, "pipe": 0x200, "generic": 0x300, "wide": 0x400, "wide16": 0x500}
+FUSED_PATH = {"auto": 0, "item": 0x100, "pipe": 0x200, "generic": 0x300, "wide": 0x400, "wide16": 0x500, "staged": 0x600}
 FUSED_ORDER = {"auto": 0, "channel": 0x1000, "xcd": 0x2000}
 
 

@@ -1177,9 +1177,10 @@ int launch_i8(FusedArgs P, hipStream_t st) {
   const int S8 = (2 * P.A + 63) / 64;
   const int choice = fused_kernel_choice(P);
   const bool small = S8 <= 2 && P.T <= 256;
-  if ((choice == BF_FUSED_PATH_WIDE || (choice == 0 && !small)) && i8_wide_lc_fits(P))
-    return launch_i8_wide_lc<Signed>(P, st);
-  if ((choice == BF_FUSED_PATH_WIDE || choice == BF_FUSED_PATH_WIDE16 || (choice == 0 && !small)) && i8_wide_fits(P))
+  if (choice == BF_FUSED_PATH_STAGED && i8_wide_lc_fits(P)) return launch_i8_wide_lc<Signed>(P, st);
+  if ((choice == BF_FUSED_PATH_WIDE || (choice == 0 && !small)) && i8_w32_fits(P)) return launch_i8_w32<Signed>(P, st);
+  if ((choice == BF_FUSED_PATH_WIDE || choice == BF_FUSED_PATH_WIDE16 || choice == BF_FUSED_PATH_STAGED ||
+       (choice == 0 && !small)) && i8_wide_fits(P))
     return launch_i8_wide<Signed>(P, st);
   if (small && choice != BF_FUSED_PATH_GENERIC) {
     const int M2 = 2 * P.M;
@@ -1309,7 +1310,7 @@ extern "C" int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay
   BF_REQUIRE((flags & ~(BF_FUSED_SIGNED | BF_FUSED_OUT_INT8 | BF_FUSED_EXACT_COEFF | BF_FUSED_INT8_VIA_F32 |
                          BF_FUSED_PATH_MASK | BF_FUSED_ORDER_MASK)) == 0,
              "bf_beamform_fused: unknown flags 0x%x", flags);
-  BF_REQUIRE((flags & BF_FUSED_PATH_MASK) <= BF_FUSED_PATH_WIDE16, "bf_beamform_fused: unknown kernel path 0x%x",
+  BF_REQUIRE((flags & BF_FUSED_PATH_MASK) <= BF_FUSED_PATH_STAGED, "bf_beamform_fused: unknown kernel path 0x%x",
              flags & BF_FUSED_PATH_MASK);
   BF_REQUIRE((flags & BF_FUSED_ORDER_MASK) != BF_FUSED_ORDER_MASK, "bf_beamform_fused: unknown workgroup order");
   BF_REQUIRE((reinterpret_cast<uintptr_t>(raw) & 15) == 0 && (reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 &&
@@ -1421,7 +1422,81 @@ __global__ __launch_bounds__(256) void stream_mix_kernel(const uint4* __restrict
       *reinterpret_cast<u32x4*>(out + i) = a;
   }
 }
+// The wide kernels' read pattern as a stream: the voltages (A, C, T*4) = rows of R = T*4 bytes per (antenna,
+// channel); item c needs row c of every antenna (stride C*R).  Pattern 0: one wave-load = one 1 KiB row piece,
+// the WG's waves take every 4th antenna; 1: w8's shape (16 lanes x 16 B of 4 antennas per wave-load); 2: a WG
+// owns `run` consecutive items and sweeps antenna-major (16 KiB contiguous per antenna at run 16).  U 16-byte loads
+// in flight per lane.  Items: the WG's `items` = C / grid.
+template <int Pattern, int U>
+__global__ __launch_bounds__(256) void item_read_kernel(const uint8_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                        int A, int C, int R) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t astride = static_cast<size_t>(C) * R;
+  const int per = C / gridDim.x;
+  u32x4 acc = {0, 0, 0, 0};
+  if constexpr (Pattern == 2) {
+    const int c0 = blockIdx.x * per;  // rows c0 .. c0 + per - 1 of each antenna are contiguous
+    const size_t span = static_cast<size_t>(per) * R / 16;  // 16-byte pieces per antenna
+    const size_t n = span * A;
+    for (size_t i0 = threadIdx.x; i0 < n; i0 += 256 * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t i = min(i0 + 256 * u, n - 1);
+        const size_t a = i / span, j = i % span;
+        v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + a * astride + static_cast<size_t>(c0) * R) + j);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc ^= v[u];
+    }
+  } else {
+    for (int k = 0; k < per; ++k) {
+      const int c = k * gridDim.x + blockIdx.x;
+      const uint8_t* item = in + static_cast<size_t>(c) * R;
+      const int rows_per_load = Pattern == 0 ? 1 : 4;
+      const int pieces = R / (Pattern == 0 ? 1024 : 256);  // per row
+      // load index L covers (antenna group, piece): 4 waves interleave
+      const int nloads = A / rows_per_load * pieces;
+      for (int l0 = wave; l0 < nloads; l0 += 4 * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int l = min(l0 + 4 * u, nloads - 1);
+          const int ag = l / pieces, pc = l % pieces;
+          size_t off;
+          if constexpr (Pattern == 0)
+            off = static_cast<size_t>(ag) * astride + pc * 1024 + lane * 16;
+          else
+            off = static_cast<size_t>(ag * 4 + (lane >> 4)) * astride + pc * 256 + (lane & 15) * 16;
+          v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(item + off));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u];
+      }
+    }
+  }
+  const uint32_t s = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
+  if (s == 0x9e3779b9u) out[blockIdx.x * 256 + threadIdx.x] = s;
+}
 }  // namespace bf
+
+// code = 10 * pattern + (U == 16 ? 2 : U == 8 ? 1 : 0) (U = 4, 8, 16); the voltages' shape (A, C, R).
+extern "C" int bf_diag_item_read(const void* in, void* out, int A, int C, int R, int grid, int code, void* stream) {
+  auto i8 = reinterpret_cast<const uint8_t*>(in);
+  auto o = reinterpret_cast<uint32_t*>(out);
+  hipStream_t st = bf::as_stream(stream);
+  switch (code) {
+#define BF_IR(P, UI, U)                                                                                        \
+  case 10 * P + UI:                                                                                            \
+    hipLaunchKernelGGL((bf::item_read_kernel<P, U>), dim3(grid), dim3(256), 0, st, i8, o, A, C, R); \
+    break;
+    BF_IR(0, 0, 4) BF_IR(0, 1, 8) BF_IR(0, 2, 16) BF_IR(1, 0, 4) BF_IR(1, 1, 8) BF_IR(1, 2, 16) BF_IR(2, 0, 4)
+    BF_IR(2, 1, 8) BF_IR(2, 2, 16)
+#undef BF_IR
+    default: return BF_ERR_ARG;
+  }
+  BF_LAUNCHED("item_read_kernel");
+}
 
 extern "C" int bf_diag_stream(const void* in, void* out, size_t in_bytes, size_t out_bytes, int grid, int unroll,
                               void* stream) {

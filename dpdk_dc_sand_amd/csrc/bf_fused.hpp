@@ -79,11 +79,15 @@ __device__ __forceinline__ void transpose_rows4(uint32_t (&v)[4]) {
 // Kernel-path override of a launch (flags & BF_FUSED_PATH_MASK): 0 automatic, else one of the BF_FUSED_PATH_* values.
 inline int fused_kernel_choice(const FusedArgs& P) { return P.path; }
 
-// Integer wide kernels: int8 beams for many antennas x beams.  bf_wide_i8lc.hip (loader/consumer, A in [32, 256],
-// M <= 64: the default) and bf_wide_i8.hip (a workgroup per 16-beam slab: larger shapes, BF_FUSED_PATH_WIDE16).
+// Integer wide kernels: int8 beams for many antennas x beams.  bf_wide_i8.hip: a workgroup per 32-beam slab (the
+// default, BF_FUSED_PATH_WIDE) or per 16-beam slab (BF_FUSED_PATH_WIDE16); bf_wide_i8lc.hip: loader/consumer waves
+// of a persistent workgroup (A in [32, 256], M <= 64: BF_FUSED_PATH_STAGED).
 bool i8_wide_fits(const FusedArgs& P);
 template <bool Signed>
 int launch_i8_wide(FusedArgs P, hipStream_t st);
+bool i8_w32_fits(const FusedArgs& P);
+template <bool Signed>
+int launch_i8_w32(FusedArgs P, hipStream_t st);
 bool i8_wide_lc_fits(const FusedArgs& P);
 template <bool Signed>
 int launch_i8_wide_lc(FusedArgs P, hipStream_t st);

@@ -186,7 +186,9 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(F
           ws[j] = 4096 - 16 * j;
         }
       } else {
-        q14_coeffs<kBatch, !(Mode & 128)>(dv, gv, valid, ch, P.ctot, P.ts, P.k, dt, P.gain, wc, ws);
+        // branch-free fast phasors (the kBatch float64 chains interleave); Mode 512: the branchy form (diagnostics)
+        q14_coeffs<kBatch, !(Mode & 128), false, (Mode & 512) == 0>(dv, gv, valid, ch, P.ctot, P.ts, P.k, dt, P.gain,
+                                                                     wc, ws);
       }
 #pragma unroll
       for (int j = 0; j < kBatch; ++j) {
@@ -341,6 +343,301 @@ int launch_w8(FusedArgs P, hipStream_t st) {
   BF_LAUNCHED("beamform_fused_i8_wide_kernel");
 }
 
+// ---- 32-beam slabs (the default integer wide kernel) -------------------------------------------------------------
+// The 16-beam kernel above re-reads each item's voltages once per slab (4x at 64 beams) with a prefetch distance of
+// one step: tools/diag_fused.py showed it latency-bound on those re-reads (no-coef, no-MFMA 442 us against a 164 us
+// read of the same bytes in the same item-major order).  Here a workgroup slab is 32 beams (the Q14 table is 64 KiB:
+// two workgroups per CU) and a wave 32 samples x 32 beams: half the voltage bytes per MFMA (each lane loads
+// 8-byte runs = 2 samples of 8 antennas), four step buffers of 16 registers (three steps in flight while one is
+// contracted), and the prefetch runs on across the wave's chunks so the next chunk's steps load under the stores.
+constexpr int kW32Beams = 32;
+
+// k-steps of 32 antennas padded to a multiple of 4 (the four-buffer rotation); padded steps have zero table rows
+__host__ __device__ inline int w32_steps(int A) { return 4 * ((((A + 31) >> 5) + 3) / 4); }
+__host__ __device__ inline size_t w32_lds_bytes(int A) {
+  return static_cast<size_t>(w32_steps(A)) * 4 * 2 * 64 * 16 + 4 * 32 * 4;
+}
+
+// One step's voltages: 8 antennas' 8-byte runs.  (Raw buffer loads with the row offsets as soffsets would save the
+// ~28 VALU of 64-bit address arithmetic per step, but their SGPRs pushed this 247-VGPR kernel into spills.)
+template <int Mode>
+__device__ __forceinline__ void w32_load(const uint8_t* __restrict__ base, size_t ant_stride, uint32_t loff, int s,
+                                         int A, uint32_t (&d)[8][2]) {
+  const int a0 = w8_step_base(s, A);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if constexpr (Mode & 8) {
+      d[q][0] = loff * 0x01010101u + s + q;
+      d[q][1] = loff * 0x01010101u + s - q;
+      continue;
+    }
+    const u32x2_t v = *reinterpret_cast<const u32x2_t*>(base + static_cast<size_t>(a0 + q) * ant_stride + loff);
+    d[q][0] = v[0];
+    d[q][1] = v[1];
+  }
+}
+
+// The step's B fragments [pol][sample] (one v_perm per dword); the voltage registers are free afterwards.
+template <bool Signed>
+__device__ __forceinline__ void w32_frags(const uint32_t (&d)[8][2], i32x4_t (&f)[2][2]) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint32_t w[4];
+#pragma unroll
+      for (int m2 = 0; m2 < 4; ++m2) {
+        uint32_t a = d[2 * m2][i], b = d[2 * m2 + 1][i];
+        if constexpr (!Signed) {  // x - 128 as int8 (128 * column sum added back at the end)
+          a ^= 0x80808080u;
+          b ^= 0x80808080u;
+        }
+        w[m2] = __builtin_amdgcn_perm(b, a, p ? kSelP1 : kSelP0);
+      }
+      f[p][i] = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]), static_cast<int>(w[3])};
+    }
+}
+
+// 32 MFMAs of one step: per tile t (16 real columns) the two limbs' A fragments from LDS, 2 pols x 2 samples.
+template <int Mode>
+__device__ __forceinline__ void w32_mfma(const int4* __restrict__ fr, int s, int lane, const i32x4_t (&f)[2][2],
+                                         i32x4_t (&hi)[2][2][4], i32x4_t (&lo)[2][2][4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int4 x0 = fr[(((s * 4 + t) * 2 + 0) * 64) + lane];
+    const int4 x1 = fr[(((s * 4 + t) * 2 + 1) * 64) + lane];
+    const i32x4_t chi = i32x4_t{x0.x, x0.y, x0.z, x0.w}, clo = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if constexpr (Mode & 2) {
+          hi[p][i][t] += f[p][i] + chi;
+          lo[p][i][t] += f[p][i] + clo;
+        } else {
+          hi[p][i][t] = mfma_i8(chi, f[p][i], hi[p][i][t]);
+          lo[p][i][t] = mfma_i8(clo, f[p][i], lo[p][i][t]);
+        }
+      }
+  }
+}
+
+// Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads.
+template <bool Signed, int Mode = 0>
+__global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(FusedArgs P) {
+  extern __shared__ __attribute__((aligned(16))) int4 lds4[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  int slab, bc;
+  if (P.xcd_order) {  // the slabs of one item back to back on one XCD: the second re-reads the voltages from L2
+    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
+    slab = local % P.nslabs;
+    bc = (local / P.nslabs) * 8 + x;
+    if (bc >= P.B * P.C) return;
+  } else {
+    slab = blockIdx.x % P.nslabs;
+    bc = blockIdx.x / P.nslabs;
+  }
+  const int b = bc / P.C, c = bc % P.C;
+  const int m0 = slab * kW32Beams;
+  const int Sp = w32_steps(P.A);
+  const int T2 = P.T >> 1;
+  const int nchunks = (T2 + 15) >> 4;               // 32-sample chunks
+  const int npasses = (nchunks + 3) >> 2;           // per wave, the same count for every wave
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  const uint32_t hoff = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride);  // < 24 * stride
+  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
+  int8_t* lb = reinterpret_cast<int8_t*>(lds4);
+  int* partial = reinterpret_cast<int*>(lb + static_cast<size_t>(Sp) * 4 * 2 * 64 * 16);  // [4 waves][32 columns]
+
+  // the voltage prefetch: step ls of chunk lchunk next; runs on from one chunk into the wave's next one
+  const int total = npasses * Sp;
+  int issued = 0, ls = 0, lchunk = wave;
+  // (past the wave's last step it repeats that step: the same, just-fetched bytes, and straight-line code)
+  auto issue = [&](uint32_t (&d)[8][2]) {
+    const uint32_t loff = hoff + static_cast<uint32_t>(min(lchunk * 16 + tl, T2 - 1)) * 8u;
+    w32_load<Mode>(base, ant_stride, loff, ls, P.A, d);
+    if (++issued < total && ++ls == Sp) {
+      ls = 0;
+      lchunk += 4;
+    }
+  };
+  uint32_t d0[8][2], d1[8][2], d2[8][2], d3[8][2];
+  issue(d0);
+  issue(d1);
+  issue(d2);
+  issue(d3);
+
+  // Q14 limbs of the slab's [[R, I], [-I, R]] blocks (as the 16-beam kernel), under the loads.  Pair e -> 4
+  // consecutive slot antennas x beam row ml = (tid >> 2) % 32, slot antenna sa0 + 8 J.
+  {
+    const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+    const double ch = static_cast<double>(P.base_ch + c);
+    const int cd = P.delay_channels == 1 ? 0 : c;
+    const int nj = 4 * Sp;  // 32 Sp slot antennas x 32 beams / 256 threads
+    int cs0 = 0, cs1 = 0;
+    const int ml = (tid >> 2) & (kW32Beams - 1);
+    const int sa0 = 4 * (tid >> 7) + (tid & 3);
+    const int m = m0 + ml;
+    const bool m_ok = m < P.M;
+    const float4* dv_row = P.dv + (static_cast<size_t>(cd) * P.M + min(m, P.M - 1)) * P.A;
+    const float* g_row = P.gain ? P.gain + static_cast<size_t>(min(m, P.M - 1)) * P.A : nullptr;
+    const int off0 = coef8_byte(2 * sa0, 2 * ml, 4, 0);
+    constexpr int kBatch = 8;
+    for (int j0 = 0; j0 < nj; j0 += kBatch) {
+      float4 dv[kBatch];
+      float gv[kBatch];
+      bool valid[kBatch];
+      int wc[kBatch], ws[kBatch];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int sa = sa0 + 8 * (j0 + j), st = sa >> 5;
+        const int a = w8_step_base(st, P.A) + (sa & 31);
+        valid[j] = j0 + j < nj && m_ok && a >= 32 * st;  // rows an earlier step already covered stay zero
+        if constexpr (Mode & 1) continue;
+        dv[j] = dv_row[min(a, P.A - 1)];
+        gv[j] = g_row ? g_row[min(a, P.A - 1)] : 1.0f;
+      }
+      if constexpr (Mode & 1) {
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+          wc[j] = valid[j] ? 8192 + 16 * j + tid : 0;
+          ws[j] = valid[j] ? 4096 - 16 * j : 0;
+        }
+      } else {
+        q14_coeffs<kBatch, true, false, true>(dv, gv, valid, ch, P.ctot, P.ts, P.k, dt, P.gain, wc, ws);
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        if (j0 + j >= nj) break;
+        const int J = j0 + j;
+        const int Wc = wc[j], Ws = ws[j], nWs = -Ws;
+        // k = 2 sa0 + 16 J: step J >> 2, lane group J & 3 (2 sa0 < 16)
+        int8_t* o = lb + off0 + 8192 * (J >> 2) + 256 * (J & 3);
+        *reinterpret_cast<uint16_t*>(o) = static_cast<uint16_t>(__builtin_amdgcn_perm(nWs + 128, Wc + 128, 0x0c0c0501u));
+        *reinterpret_cast<uint16_t*>(o + 64 * 16) = static_cast<uint16_t>(__builtin_amdgcn_perm(nWs, Wc, 0x0c0c0400u));
+        *reinterpret_cast<uint16_t*>(o + 16) = static_cast<uint16_t>(__builtin_amdgcn_perm(Wc + 128, Ws + 128, 0x0c0c0501u));
+        *reinterpret_cast<uint16_t*>(o + 16 + 64 * 16) = static_cast<uint16_t>(__builtin_amdgcn_perm(Wc, Ws, 0x0c0c0400u));
+        cs0 += Wc - Ws;
+        cs1 += Ws + Wc;
+      }
+    }
+    if constexpr (!Signed) {
+      cs0 += __shfl_xor(cs0, 1);
+      cs1 += __shfl_xor(cs1, 1);
+      cs0 += __shfl_xor(cs0, 2);
+      cs1 += __shfl_xor(cs1, 2);
+      if ((lane & 3) == 0) {  // wave w holds columns 32 (w & 1) + [0, 32)
+        partial[wave * 32 + 2 * (lane >> 2)] = cs0;
+        partial[wave * 32 + 2 * (lane >> 2) + 1] = cs1;
+      }
+    }
+  }
+  __syncthreads();
+
+  const float s32 = P.out_scale * 0x1p-14f;
+  const int M2 = 2 * P.M;
+  const bool full = m0 + kW32Beams <= P.M && (M2 & 15) == 0;  // 16-byte row pieces (uniform)
+  int chunk = wave;
+  for (int pass = 0; pass < npasses; ++pass) {
+    const int tq = chunk * 16 + tl;  // sample pair
+    i32x4_t hi[2][2][4], lo[2][2][4];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) hi[p][i][t] = lo[p][i][t] = i32x4_t{0, 0, 0, 0};
+    // four steps in flight; a step's buffer is reloaded as soon as its fragments are built
+    for (int s = 0; s < Sp; s += 4) {
+      i32x4_t f[2][2];
+      w32_frags<Signed>(d0, f);
+      issue(d0);
+      w32_mfma<Mode>(lds4, s, lane, f, hi, lo);
+      w32_frags<Signed>(d1, f);
+      issue(d1);
+      w32_mfma<Mode>(lds4, s + 1, lane, f, hi, lo);
+      w32_frags<Signed>(d2, f);
+      issue(d2);
+      w32_mfma<Mode>(lds4, s + 2, lane, f, hi, lo);
+      w32_frags<Signed>(d3, f);
+      issue(d3);
+      w32_mfma<Mode>(lds4, s + 3, lane, f, hi, lo);
+    }
+    if constexpr (Mode & 4) {
+      int sum = 0;
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) sum += hi[p][i][t][0] ^ lo[p][i][t][3];
+      if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[tid] = sum;
+    } else {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint32_t pk[2][4];  // [sample i][tile t] -> 4 packed int8 columns 16 t + 4 h + r
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            uint32_t qb[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              int y = (hi[p][i][t][r] << 8) + lo[p][i][t][r];
+              if constexpr (!Signed) {  // unsigned samples: 128 * the column sum (two wave partials)
+                const int cl = 16 * t + 4 * h + r;
+                y += 128 * (partial[(cl >> 5) * 32 + (cl & 31)] + partial[((cl >> 5) + 2) * 32 + (cl & 31)]);
+              }
+              qb[r] = requant_bits(y, s32);
+            }
+            pk[i][t] = pack_low_bytes(qb[0], qb[1], qb[2], qb[3]);
+          }
+        const size_t prow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T);
+        if (full) {
+          // 4x4 transpose over (h, t): lane (tl, h) gets columns 16 h .. 16 h + 15 of sample 2 tq + i
+#pragma unroll
+          for (int i = 0; i < 2; ++i) transpose_rows4(pk[i]);
+          if (tq < T2) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 2 * tq + i) * M2 + 2 * m0 + 16 * h;
+              *reinterpret_cast<u32x4_t*>(o) = u32x4_t{pk[i][0], pk[i][1], pk[i][2], pk[i][3]};
+            }
+          }
+        } else if (tq < T2) {  // partial slab / unaligned rows: byte stores with the beam guard
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 2 * tq + i) * M2 + 2 * m0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int col = 16 * t + 4 * h + r;
+                if (2 * m0 + col < M2) o[col] = static_cast<int8_t>((pk[i][t] >> (8 * r)) & 255);
+              }
+          }
+        }
+      }
+    }
+    chunk += 4;
+  }
+}
+
+template <bool Signed, int Mode = 0>
+int launch_w32(FusedArgs P, hipStream_t st) {
+  const size_t lds = w32_lds_bytes(P.A);
+  BF_REQUIRE(lds <= kMaxLds, "bf_beamform_fused: n_ants=%d too large for the integer wide kernel", P.A);
+  P.nslabs = (P.M + kW32Beams - 1) / kW32Beams;
+  P.xcd_order = P.nslabs > 1 && P.order != BF_FUSED_ORDER_CHANNEL;
+  const long long items = static_cast<long long>(P.B) * P.C;
+  const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
+  BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
+  hipLaunchKernelGGL((beamform_fused_i8_w32_kernel<Signed, Mode>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kW8Threads), lds, st, P);
+  BF_LAUNCHED("beamform_fused_i8_w32_kernel");
+}
+
 }  // namespace
 
 bool i8_wide_fits(const FusedArgs& P) {
@@ -349,13 +646,26 @@ bool i8_wide_fits(const FusedArgs& P) {
   return P.A >= 32 && 24 * ant_stride + static_cast<size_t>(P.T) * 4 < (1ull << 32) && lds <= kMaxLds;
 }
 
+bool i8_w32_fits(const FusedArgs& P) {
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  return P.A >= 32 && (P.T & 1) == 0 && 24 * ant_stride + static_cast<size_t>(P.T) * 4 < (1ull << 32) &&
+         w32_lds_bytes(P.A) <= kMaxLds;
+}
+
 template <bool Signed>
 int launch_i8_wide(FusedArgs P, hipStream_t st) {
   return launch_w8<Signed>(P, st);
 }
 
+template <bool Signed>
+int launch_i8_w32(FusedArgs P, hipStream_t st) {
+  return launch_w32<Signed>(P, st);
+}
+
 template int launch_i8_wide<false>(FusedArgs, hipStream_t);
 template int launch_i8_wide<true>(FusedArgs, hipStream_t);
+template int launch_i8_w32<false>(FusedArgs, hipStream_t);
+template int launch_i8_w32<true>(FusedArgs, hipStream_t);
 
 }  // namespace bf
 
@@ -395,7 +705,17 @@ extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y
     case 256 + 3: return bf::launch_w8<true, 256 + 3>(P, st);
     case 256 + 16 + 3: return bf::launch_w8<true, 256 + 16 + 3>(P, st);
     case 256: return bf::launch_w8<true, 256>(P, st);
+    case 512: return bf::launch_w8<true, 512>(P, st);
     case 128: return bf::launch_w8<true, 128>(P, st);  // exact phasors only (no fast attempt)
+    // 32-beam slabs: 1000 + the kernel's Mode bits
+    case 1000: return bf::launch_w32<true, 0>(P, st);
+    case 1001: return bf::launch_w32<true, 1>(P, st);
+    case 1002: return bf::launch_w32<true, 2>(P, st);
+    case 1003: return bf::launch_w32<true, 3>(P, st);
+    case 1004: return bf::launch_w32<true, 4>(P, st);
+    case 1008: return bf::launch_w32<true, 8>(P, st);
+    case 1009: return bf::launch_w32<true, 9>(P, st);
+    case 1013: return bf::launch_w32<true, 13>(P, st);
     default: return BF_ERR_ARG;
   }
 }

@@ -74,6 +74,25 @@ __device__ __forceinline__ void lc_wait(const unsigned* ctr, unsigned target) {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+// Diagnostics (Mode & 16): per-wave cycle counters by phase, summed with s_memtime and written over the output
+// buffer at the end (loader: 0 total, 1 table units, 2 slot waits, 3 ring writes; consumer: 0 total, 1 table waits,
+// 2 slot waits, 3 steps, 4 stores).
+struct LcStamps {
+  unsigned long long v[5] = {0, 0, 0, 0, 0};
+  unsigned long long t0 = 0;
+  __device__ void start() { t0 = __builtin_amdgcn_s_memtime(); }
+  __device__ void lap(int i) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    v[i] += t - t0;
+    t0 = t;
+  }
+  __device__ void flush(void* y, int wave) {
+    unsigned long long* o = reinterpret_cast<unsigned long long*>(y) + (blockIdx.x * 8 + wave) * 8;
+    if ((threadIdx.x & 63) == 0)
+      for (int i = 0; i < 5; ++i) o[i] = v[i];
+  }
+};
+
 // Per-workgroup item run: XCD x = blockIdx % 8 owns items [x n8, (x+1) n8) (n8 = ceil(B C / 8)); its L workgroups
 // take them round-robin, so an XCD's resident workgroups stream adjacent channels of every antenna row.
 struct LcRun {
@@ -334,6 +353,9 @@ __device__ __forceinline__ void lc_loader(const FusedArgs& P, const LcRun& run, 
                                           const LcLayout& L, int nact, int w, int lane) {
   const int tl = lane & 15, qq = lane >> 4;
   const int per_item = NQ * S;
+  LcStamps st;
+  const unsigned long long tbeg = __builtin_amdgcn_s_memtime();
+  if constexpr ((Mode & 16) != 0) st.start();
   LcLoad R[kLcDepth];
   LcCursor u{0, 0, 0, 0, lc_item_base(P, run, 0)};
 #pragma unroll
@@ -361,16 +383,20 @@ __device__ __forceinline__ void lc_loader(const FusedArgs& P, const LcRun& run, 
       int budget = upt;
       for (int n = 0; n < kLcSpinCap; ++n) {
         if (T.done && T.k + 1 < run.count) lc_tstart(P, run, S, w, T.k + 1, lane, T);
+        if constexpr ((Mode & 16) != 0) st.lap(2);
         const bool did = lc_try_table<Mode>(P, run, S, w, lane, L, nact, T);
+        if constexpr ((Mode & 16) != 0) st.lap(did ? 1 : 2);
         if (did && --budget > 0) continue;
         if (lc_ready(L.ctr + 4 + slot, static_cast<unsigned>(nact * (t / kLcRing)))) break;
         if (!did) __builtin_amdgcn_s_sleep(1);
       }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if constexpr ((Mode & 16) != 0) st.lap(2);
       lc_write<Signed>(L.ring + slot * kLcSlot, w, tl, qq, R[kk]);
       lc_issue<Mode>(P, u, w, tl, qq, R[kk]);  // step t + kLcDepth (clamped)
       lc_advance(P, run, S, NQ, nsteps, u);
       lc_signal(L.ctr + slot);
+      if constexpr ((Mode & 16) != 0) st.lap(3);
     }
   }
   for (int n = 0; n < kLcSpinCap; ++n) {  // the remaining tables
@@ -379,6 +405,10 @@ __device__ __forceinline__ void lc_loader(const FusedArgs& P, const LcRun& run, 
       lc_tstart(P, run, S, w, T.k + 1, lane, T);
     }
     if (!lc_try_table<Mode>(P, run, S, w, lane, L, nact, T)) __builtin_amdgcn_s_sleep(1);
+  }
+  if constexpr ((Mode & 16) != 0) {
+    st.v[0] = __builtin_amdgcn_s_memtime() - tbeg;
+    st.flush(P.y, 4 + w);
   }
 }
 
@@ -462,6 +492,9 @@ template <bool Signed, int Mode>
 __device__ __forceinline__ void lc_consumer(const FusedArgs& P, const LcRun& run, int S, int NQ, int nsteps,
                                             const LcLayout& L, int slab, int lane) {
   const int h = lane >> 4;
+  LcStamps st;
+  const unsigned long long tbeg = __builtin_amdgcn_s_memtime();
+  if constexpr ((Mode & 16) != 0) st.start();
   LcFrags Fc, Fn;
   int t = 0;
   lc_wait(L.ctr, kLcLoaders);  // step 0's slot is written
@@ -470,7 +503,9 @@ __device__ __forceinline__ void lc_consumer(const FusedArgs& P, const LcRun& run
     int b, c;
     lc_item_bc(P, run, k, &b, &c);
     const int buf = k & 1;
+    if constexpr ((Mode & 16) != 0) st.lap(3);
     lc_wait(L.ctr + 8 + buf, static_cast<unsigned>(kLcLoaders * ((k >> 1) + 1)));  // every slab of item k is tabled
+    if constexpr ((Mode & 16) != 0) st.lap(1);
     const int8_t* table = L.table(buf) + slab * S * kLcStepTable;
     int corr[2][4];  // [re / im][beam 4 h + r]
 #pragma unroll
@@ -493,7 +528,9 @@ __device__ __forceinline__ void lc_consumer(const FusedArgs& P, const LcRun& run
       for (int s = 0; s < S; ++s, ++t) {
         if (t > 0) lc_add(L.ctr + 4 + (t - 1) % kLcRing);  // slot t - 1 was consumed by the last step's MFMAs
         const int tn = t + 1 < nsteps ? t + 1 : t;          // the last prefetch re-reads a slot it holds (unused)
+        if constexpr ((Mode & 16) != 0) st.lap(3);
         lc_wait(L.ctr + tn % kLcRing, static_cast<unsigned>(kLcLoaders * (tn / kLcRing + 1)));
+        if constexpr ((Mode & 16) != 0) st.lap(2);
         lc_read_frags(L.ring + (tn % kLcRing) * kLcSlot, lane, Fn);
         i32x4_t nhi = ahi, nlo = alo;
         if (s + 1 < S) lc_read_table(table + (s + 1) * kLcStepTable, lane, nhi, nlo);
@@ -528,11 +565,17 @@ __device__ __forceinline__ void lc_consumer(const FusedArgs& P, const LcRun& run
             for (int ri = 0; ri < 2; ++ri) sum += acc.hi[p][i][ri][0] ^ acc.lo[p][i][ri][3];
         if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[lane] = sum;
       } else {
+        if constexpr ((Mode & 16) != 0) st.lap(3);
         lc_store_quarter<Signed>(P, b, c, q, 16 * slab, lane, acc, corr);
+        if constexpr ((Mode & 16) != 0) st.lap(4);
       }
       if (q + 1 < NQ) lc_read_table(table, lane, ahi, alo);  // step 0 again for the next quarter
     }
     lc_signal(L.ctr + 10 + buf);  // the table buffer of item k is free
+  }
+  if constexpr ((Mode & 16) != 0) {
+    st.v[0] = __builtin_amdgcn_s_memtime() - tbeg;
+    st.flush(P.y, slab);
   }
 }
 
@@ -632,6 +675,8 @@ extern "C" int bf_diag_lc(int mode, const uint8_t* raw, const float* dv, void* y
     case 9: return bf::launch_lc<true, 9>(P, st);
     case 11: return bf::launch_lc<true, 11>(P, st);
     case 15: return bf::launch_lc<true, 15>(P, st);
+    case 16: return bf::launch_lc<true, 16>(P, st);
+    case 17: return bf::launch_lc<true, 17>(P, st);
     default: return BF_ERR_ARG;
   }
 }

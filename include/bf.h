@@ -126,7 +126,8 @@ int bf_beamform(const uint8_t* x, const float* w, float* y, int B, int P, int C,
 #define BF_FUSED_PATH_PIPE 0x0200    /* persistent double-buffered item kernel (float beams) */
 #define BF_FUSED_PATH_GENERIC 0x0300 /* any A, any T: groups of 64 antennas */
 #define BF_FUSED_PATH_WIDE 0x0400    /* many antennas x beams: multi-wave beam slabs (config 4) */
-#define BF_FUSED_PATH_WIDE16 0x0500  /* the float wide kernel with 16-beam slabs */
+#define BF_FUSED_PATH_WIDE16 0x0500  /* 16-beam slabs (float and int8 wide kernels) */
+#define BF_FUSED_PATH_STAGED 0x0600  /* int8 beams: loader/consumer waves of a persistent workgroup (A <= 256, M <= 64) */
 #define BF_FUSED_ORDER_MASK 0x3000
 #define BF_FUSED_ORDER_CHANNEL 0x1000 /* plain channel-fastest workgroup order */
 #define BF_FUSED_ORDER_XCD 0x2000     /* XCD-range order (XCD x streams channels [x C/8, (x+1) C/8)) */

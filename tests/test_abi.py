@@ -93,7 +93,7 @@ def test_kernel_path_and_contract_flags_are_validated():
     fake = 1 << 20
     args = [fake, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0]
     with pytest.raises(_lib.BeamformerError, match="unknown kernel path"):
-        _lib.call("bf_beamform_fused", *args, 0x600, 1.0, None)
+        _lib.call("bf_beamform_fused", *args, 0x700, 1.0, None)
     with pytest.raises(_lib.BeamformerError, match="unknown workgroup order"):
         _lib.call("bf_beamform_fused", *args, 0x3000, 1.0, None)
     # Q14 int8 contract: more uint8 antennas than the int32 beam sums hold (A * 255 * 23171 >= 2^31) is refused

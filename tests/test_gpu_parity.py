@@ -302,7 +302,7 @@ def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C
     (4, 1, 16, 1024, 1, 16, True), (80, 24, 3, 16, 3, 1, True), (32, 8, 4, 64, 2, 1, False),
     (48, 12, 2, 128, 2, 1, False), (33, 5, 3, 80, 2, 3, True), (16, 8, 3, 48, 2, 1, True),
     (64, 16, 2, 112, 1, 1, False), (40, 32, 2, 64, 1, 2, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16", "staged"])
 def test_fused_int8_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """int8 (requantised) beams: the integer MFMA path reproduces the oracle's integer contract bit for bit, on the
     item kernel (A <= 64, T <= 256; others fall through to generic) and the generic kernel (any A, T)."""
@@ -436,7 +436,7 @@ def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, 
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
     (64, 16, 3, 256, 2, 1, True), (64, 16, 2, 256, 2, 1, False), (19, 3, 4, 48, 2, 4, False),
     (130, 9, 2, 64, 1, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16", "staged"])
 def test_fused_int8_beam_weights_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """Weighted int8 beams: Q14 limbs of the weighted float32 coefficients, bit-exact to the integer contract."""
     Ctot, xeng, t0, bdt = 4096, 2, 1e-3, 256 * 8192 * TS
@@ -475,7 +475,7 @@ def boundary_delays(M, A, seed):
 
 @pytest.mark.parametrize("A,M,C,T,B,signed", [(64, 16, 3, 256, 2, True), (64, 16, 2, 256, 2, False),
                                               (19, 3, 3, 48, 2, False), (256, 64, 1, 32, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16", "staged"])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_fused_int8_rounding_boundaries(context, command_queue, i8_kernel, weighted, A, M, C, T, B,
                                         signed):

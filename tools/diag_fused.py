@@ -78,7 +78,9 @@ if "w8" in _os.environ.get("DIAG_KERNELS", ""):
                19: "slab0 only,no-coef,no-mfma", 35: "nt loads,no-coef,no-mfma", 51: "slab0,nt,no-coef,no-mfma",
                32: "nt loads (full)", 17: "slab0 only,no-coef", 67: "16 ant rows,no-coef,no-mfma",
                83: "16 rows,slab0,no-coef,no-mfma", 259: "xcd-range,no-coef,no-mfma", 275: "xcd-range,slab0,nc,nm",
-               256: "xcd-range (full)"}
+               256: "xcd-range (full)", 512: "branchy phasors (old)",
+               1000: "w32 full", 1001: "w32 no-coef", 1002: "w32 no-mfma", 1003: "w32 no-coef,no-mfma",
+               1004: "w32 no-store", 1008: "w32 no-load", 1009: "w32 no-coef,no-load", 1013: "w32 nc,nl,ns"}
     if _os.environ.get("W8_MODES"):
         w8names = {int(m): w8names.get(int(m), str(m)) for m in _os.environ["W8_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
@@ -106,6 +108,8 @@ if "lc" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_lc.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
     lcnames = {0: "full", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store", 8: "no-load",
                9: "no-coef,no-load", 11: "no-coef,no-mfma,no-load", 15: "barriers+lds only"}
+    if _os.environ.get("LC_MODES"):
+        lcnames = {int(m): lcnames.get(int(m), str(m)) for m in _os.environ["LC_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
     alg8 = nin + nout // 4 // 4
     res = {m: [] for m in lcnames}
@@ -117,6 +121,15 @@ if "lc" in _os.environ.get("DIAG_KERNELS", ""):
         ts = sorted(res[mode])
         print(f"  lc mode {mode:2d} {lcnames[mode]:26s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
               f"alg {alg8 / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
+    for smode in (16, 17):  # phase stamps (s_memtime cycles per wave, averaged over workgroups)
+        q.finish()
+        assert lib.bf_diag_lc(smode, bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, B, C, T, A, M, Ctot, 1 / 1712e6, q.handle) == 0
+        q.finish()
+        raw = bufs[0][1].get(q)[: 256 * 8 * 8 * 8].view(np.uint64).reshape(256, 8, 8).astype(np.float64)
+        cons, lod = raw[:, :4, :5].mean(axis=(0, 1)), raw[:, 4:, :4].mean(axis=(0, 1))
+        print(f"  lc stamps mode {smode}: consumer total {cons[0]:.0f} cyc: table-wait {cons[1]:.0f} slot-wait "
+              f"{cons[2]:.0f} steps {cons[3]:.0f} stores {cons[4]:.0f} | loader total {lod[0]:.0f}: table {lod[1]:.0f} "
+              f"slot-wait {lod[2]:.0f} ring {lod[3]:.0f}")
 names_i8 = {0: "full (fast+fixup coef, occ 3)", 128: "exact-only coef", 16: "fast coef (inexact)", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store",
             5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
             65: "occ 2, no-store", 1024: "serial coef", 2048: "pol order", 3072: "serial+pol order",
@@ -165,3 +178,14 @@ if _os.environ.get("DIAG_STREAMS", "1") == "1":
                 t = timeit(lambda i: lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, ri, wo, grid, unroll,
                                                         q.handle))
                 print(f"  stream grid {grid:5d} {uname:8s} {nm:11s} {t*1e6:8.1f} us  {(ri + wo)/t/1e9:7.1f} GB/s")
+if _os.environ.get("DIAG_ITEMREAD"):  # the wide kernels' item-major read pattern vs an antenna-major sweep
+    lib.bf_diag_item_read.argtypes = [V, V, I, I, I, I, I, V]
+    R = T * 4
+    t = timeit(lambda i: lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, nin, 0, 2048, 102, q.handle))
+    print(f"  linear nt-load read-only   {t*1e6:8.1f} us  {nin/t/1e9:7.1f} GB/s")
+    for pat, pname in ((0, "item, 1 KiB rows"), (1, "item, w8 4x256 B"), (2, "run, antenna-major")):
+        for grid in (256, 512, 1024):
+            for ui, u in ((0, 4), (1, 8), (2, 16)):
+                t = timeit(lambda i: lib.bf_diag_item_read(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, A, C, R, grid,
+                                                           10 * pat + ui, q.handle))
+                print(f"  item-read {pname:20s} grid {grid:5d} U {u:2d} {t*1e6:8.1f} us  {nin/t/1e9:7.1f} GB/s")
