@@ -443,7 +443,7 @@ def kernel_name(wl, out_int8, int8_contract="q14"):
     integer = out_int8 and int8_contract == "q14"
     if wl["A"] <= 64 and wl["T"] <= 256:
         return "beamform_fused_i8_item_kernel" if integer else "beamform_fused_item_kernel"
-    return "beamform_fused_i8_wide_kernel" if integer else "beamform_fused_wide_kernel"
+    return "beamform_fused_i8_w32_kernel" if integer else "beamform_fused_wide_kernel"
 
 
 def secondary(args, dist, workload, out_int8, int8_contract="q14"):

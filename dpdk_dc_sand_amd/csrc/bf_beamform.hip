@@ -73,6 +73,21 @@ __device__ __forceinline__ void stage_table(_Float16* lh, const float* __restric
   }
 }
 
+// Workgroup -> (item bpc, slab).  xcd: the slabs of one item run back to back on one XCD (workgroups are dealt to
+// the 8 XCDs round-robin), so the slabs after the first re-read the item's voltages from that XCD's L2; the grid is
+// padded to whole groups of 8 items and the padding workgroups return at once.
+__device__ __forceinline__ bool table_coords(int nslabs, long long nbpc, int xcd, int& slab, size_t& bpc) {
+  if (xcd) {
+    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
+    slab = local % nslabs;
+    bpc = static_cast<size_t>(local / nslabs) * 8 + x;
+    return static_cast<long long>(bpc) < nbpc;
+  }
+  slab = blockIdx.x % nslabs;
+  bpc = blockIdx.x / nslabs;
+  return true;
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // MatrixMultiply drop-in.  grid = B*P*C*nslabs; a slab is NTS 16-column tiles of the 2M outputs.
 // Vec8: A % 4 == 0, so a lane's 8 bytes are one aligned 8-byte load; otherwise 2-byte antenna granules.
@@ -80,11 +95,12 @@ template <bool Signed, int NTS, bool Vec8>
 __global__ __launch_bounds__(kThreads) void beamform_table_kernel(const uint8_t* __restrict__ x,
                                                                   const float* __restrict__ w,
                                                                   float* __restrict__ y, int NB, int A, int M, int S,
-                                                                  int NT, int nslabs) {
+                                                                  int NT, int nslabs, long long nbpc, int xcd) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int slab = blockIdx.x % nslabs;
-  const size_t bpc = blockIdx.x / nslabs;
+  int slab;
+  size_t bpc;
+  if (!table_coords(nslabs, nbpc, xcd, slab, bpc)) return;
   const int tau0 = slab * NTS;
   const int nts = min(NTS, NT - tau0);
   const int K2 = 2 * A, M2 = 2 * M;
@@ -154,11 +170,13 @@ template <bool Signed, int NTS, int R>
 __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uint8_t* __restrict__ x,
                                                                        const float* __restrict__ w,
                                                                        float* __restrict__ y, int NB, int A, int M,
-                                                                       int S, int NT, int nslabs) {
+                                                                       int S, int NT, int nslabs, long long nbpc,
+                                                                       int xcd) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int slab = blockIdx.x % nslabs;
-  const size_t bpc = blockIdx.x / nslabs;
+  int slab;
+  size_t bpc;
+  if (!table_coords(nslabs, nbpc, xcd, slab, bpc)) return;
   const int tau0 = slab * NTS;
   const int nts = min(NTS, NT - tau0);
   const int K2 = 2 * A, M2 = 2 * M;
@@ -227,10 +245,11 @@ int launch_table(const uint8_t* x, const float* w, float* y, long long bpc, int 
   const int nslabs = (NT + NTS - 1) / NTS;
   const size_t lds = coef_lds_bytes(S, NTS);
   BF_REQUIRE(lds <= kMaxLds, "bf_beamform: n_ants=%d too large for one coefficient slab", A);
-  const long long grid = bpc * nslabs;
+  const int xcd = nslabs > 1;
+  const long long grid = xcd ? (bpc + 7) / 8 * 8 * nslabs : bpc * nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform: grid too large");
   hipLaunchKernelGGL((beamform_table_kernel<Signed, NTS, Vec8>), dim3(static_cast<unsigned>(grid)), dim3(kThreads),
-                     lds, st, x, w, y, NB, A, M, S, NT, nslabs);
+                     lds, st, x, w, y, NB, A, M, S, NT, nslabs, bpc, xcd);
   BF_LAUNCHED("beamform_table_kernel");
 }
 
@@ -241,10 +260,11 @@ int launch_ring(const uint8_t* x, const float* w, float* y, long long bpc, int N
   const int Sp = (S + R - 1) / R * R;
   const size_t lds = coef_lds_bytes(Sp, NTS);
   BF_REQUIRE(lds <= kMaxLds, "bf_beamform: n_ants=%d too large for one coefficient slab", A);
-  const long long grid = bpc * nslabs;
+  const int xcd = nslabs > 1;
+  const long long grid = xcd ? (bpc + 7) / 8 * 8 * nslabs : bpc * nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform: grid too large");
   hipLaunchKernelGGL((beamform_table_ring_kernel<Signed, NTS, R>), dim3(static_cast<unsigned>(grid)), dim3(kThreads),
-                     lds, st, x, w, y, NB, A, M, S, NT, nslabs);
+                     lds, st, x, w, y, NB, A, M, S, NT, nslabs, bpc, xcd);
   BF_LAUNCHED("beamform_table_ring_kernel");
 }
 
@@ -270,7 +290,17 @@ int dispatch_vec(const uint8_t* x, const float* w, float* y, long long bpc, int 
 template <bool Signed>
 int dispatch_table(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                    hipStream_t st) {
-  // Widest slab whose fragments fit LDS (fewer slabs = fewer re-reads of x).
+  // Long rows (>= 16 k-steps: 256+ antennas): the widest slab whose staged fragments leave room for a second
+  // workgroup per CU, so one workgroup's table staging overlaps the other's contraction (cfg4: a 128 KiB slab held
+  // one workgroup per CU and ran 3.1 ms); the slabs' re-reads of x hit L2 (XCD-grouped slabs).
+  if (S >= 16) {
+    const size_t half = kMaxLds / 2;
+    if (NT >= 4 && coef_lds_bytes((S + 15) / 16 * 16, 4) <= half)
+      return dispatch_vec<Signed, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
+    if (NT >= 2 && coef_lds_bytes((S + 15) / 16 * 16, 2) <= half)
+      return dispatch_vec<Signed, 2>(x, w, y, bpc, NB, A, M, S, NT, st);
+  }
+  // Otherwise the widest slab whose fragments fit LDS (fewer slabs = fewer re-reads of x).
   if (NT >= 8 && coef_lds_bytes(S, 8) <= kMaxLds) return dispatch_vec<Signed, 8>(x, w, y, bpc, NB, A, M, S, NT, st);
   if (NT >= 4 && coef_lds_bytes(S, 4) <= kMaxLds) return dispatch_vec<Signed, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
   if (NT >= 2 && coef_lds_bytes(S, 2) <= kMaxLds) return dispatch_vec<Signed, 2>(x, w, y, bpc, NB, A, M, S, NT, st);

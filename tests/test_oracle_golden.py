@@ -122,3 +122,22 @@ def test_beam_weights_oracle_properties():
     np.testing.assert_array_equal(diff[..., :4], 0)
     q1 = O.fused_beamform_int8(raw, d, 64, scale=1 / 16)
     np.testing.assert_array_equal(O.fused_beamform_int8(raw, d, 64, scale=1 / 16, gains=np.ones((4, 6), np.float32)), q1)
+
+
+def test_reference_bar_arbitration_path():
+    """assert_reference_bar's fallback for elements that miss rtol=atol=1e-4 (taken on the GPU only when a beam
+    cancels to near zero): a miss that is exact against the float64 product passes, one that is not fails."""
+    import pytest
+    from tolerance import assert_reference_bar
+    rng = np.random.default_rng(3)
+    B, P, C, NB, A, M = 1, 2, 3, 2, 5, 2
+    x = rng.integers(0, 256, (B, P, C, NB, 16, A, 2), dtype=np.uint8)
+    w = rng.uniform(-1, 1, (B, P, C, 2 * A, 2 * M)).astype(np.float32)
+    exact = O.complex_mult(x, w).astype(np.float64)
+    ref = exact.copy()
+    ref.reshape(-1)[7] += 1.0  # the "reference f32" result is off at one element; the GPU result is exact there
+    assert assert_reference_bar(exact, ref, x, w) == 1
+    bad = exact.copy()
+    bad.reshape(-1)[7] += 2.0  # farther from the exact product than the reference, outside the bar and the fp32 bound
+    with pytest.raises(AssertionError):
+        assert_reference_bar(bad, ref, x, w)

@@ -10,6 +10,7 @@ So the contract adds the fp32 dot-product term: two fp32 evaluations of y = sum_
 import numpy as np
 
 import oracle as O
+from oracle.beamform_oracle import _as_real
 
 RTOL = 1e-4
 ATOL = 1e-4
@@ -44,7 +45,10 @@ def assert_reference_bar(actual, desired, x_reordered, w, signed=False, max_frac
     That CPU result is itself rounded at the scale of its partial sums (|partial| ~ 1e3 -> ulp ~ 1e-4), so an output
     that cancels to near zero can sit 1e-4 from the exact value on the CPU side alone.  Every element that misses the
     bar must therefore (a) meet the same bar against the exact (float64) product, or (b) be no farther from the exact
-    product than the reference's float32 result is; and such elements must be rare (<= max_fraction).
+    product than the reference's float32 result is, or (c) lie within the float32 dot-product rounding bound
+    2^-20 * sum_k |x_k w_k| of the exact product (the same accumulation-order term as assert_beams_allclose: an fp32
+    sum whose partials reach ~1e3 can land 1e-4 from a near-zero exact result in either implementation); and such
+    elements must be rare (<= max_fraction).
     Returns the number of elements that missed the plain bar (reported by the caller)."""
     a = np.asarray(actual, np.float64)
     d = np.asarray(desired, np.float64)
@@ -56,14 +60,17 @@ def assert_reference_bar(actual, desired, x_reordered, w, signed=False, max_frac
     assert n <= max(1, max_fraction * a.size), f"{n}/{a.size} beams miss the reference's rtol=atol=1e-4 bar"
     # exact products of the missing elements only: a = (B, P, C, NB, 16, 2M) <-> x (B, P, C, NB, 16, A, 2), w (B,P,C,2A,2M)
     B, P, C, NB, S, A, Z = x_reordered.shape
-    X = O._as_real(x_reordered, signed).reshape(B, P, C, NB * S, 2 * A).astype(np.float64)
+    X = _as_real(x_reordered, signed).reshape(B, P, C, NB * S, 2 * A).astype(np.float64)
     W = np.asarray(w, np.float64)
     for idx in zip(*np.nonzero(miss.reshape(B, P, C, NB * S, -1))):
         b, p, c, t, col = (int(v) for v in idx)
         exact = float(np.dot(X[b, p, c, t], W[b, p, c, :, col]))
+        mag = float(np.dot(np.abs(X[b, p, c, t]), np.abs(W[b, p, c, :, col])))
         got = float(a.reshape(B, P, C, NB * S, -1)[b, p, c, t, col])
         ref = float(d.reshape(B, P, C, NB * S, -1)[b, p, c, t, col])
-        ok = abs(got - exact) <= ATOL + RTOL * abs(exact) or abs(got - exact) <= abs(ref - exact)
-        assert ok, (f"beam {idx}: gpu {got!r}, reference f32 {ref!r}, exact {exact!r}: the GPU misses the bar against "
-                    "the exact product and is farther from it than the reference's own float32 result")
+        err = abs(got - exact)
+        ok = err <= ATOL + RTOL * abs(exact) or err <= abs(ref - exact) or err <= 2.0 ** -20 * mag
+        assert ok, (f"beam {idx}: gpu {got!r}, reference f32 {ref!r}, exact {exact!r}, sum|x w| {mag!r}: the GPU "
+                    "misses the bar against the exact product, is farther from it than the reference's own float32 "
+                    "result and outside the fp32 dot-product rounding bound")
     return n
