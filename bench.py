@@ -386,7 +386,10 @@ def cpu_baseline(wl, out_int8, seconds=10.0):
 
 def pmc_traffic(args):
     """HBM bytes per fused launch from rocprofv3 counters: FETCH_SIZE and WRITE_SIZE in separate passes
-    (MI355X_MICROARCH.md: gfx950 FETCH_SIZE reads 1/2 of a wide coalesced stream -> x2; WRITE_SIZE exact; KiB)."""
+    (MI355X_MICROARCH.md: gfx950 FETCH_SIZE reads 1/2 of a wide coalesced stream -> x2; WRITE_SIZE exact; KiB).
+    Calibrated in-repo (tools/pmc_calibrate.py, profiles/r2_v_pmc_calibration.jsonl): a 1 GiB streaming read gives
+    FETCH_SIZE = 0.500 x the bytes (every request a 128-byte TCC_EA0_RDREQ_128B, tallied at 64 B), a 1 GiB write
+    WRITE_SIZE = 1.000 x, and a 1 GiB + 256 MiB mix the same two ratios."""
     exe = "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
         return None, "rocprofv3 not found"

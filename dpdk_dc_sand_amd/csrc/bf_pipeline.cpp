@@ -9,13 +9,16 @@
 //   H2D(n)     waits for compute(n - depth) (the slot's input buffer is free again);
 //   compute(n) waits for H2D(n) and for D2H(n - depth) (the slot's output buffer has been drained);
 //   D2H(n)     waits for compute(n).
-// Delay-model and beam-weight updates are staged through pinned memory and uploaded on the compute stream, so a
-// frame submitted before an update uses the old model and every later frame the new one (stream order), with no
-// host synchronisation on the data path.
+// Delay-model and beam-weight updates are staged through a ring of pinned buffers and uploaded on the compute
+// stream, so a frame submitted before an update uses the old model and every later frame the new one (stream
+// order), with no host synchronisation on the data path (an update waits only when kStage earlier updates are
+// still queued behind in-flight frames).
 #include <cstring>
 #include <vector>
 
 #include "bf_common.hpp"
+
+constexpr int kStage = 4;  // control-update staging buffers per table
 
 struct bf_pipeline {
   int B, C, T, A, M, Ctot, xeng_id, flags, delay_channels, depth, device;
@@ -27,10 +30,13 @@ struct bf_pipeline {
   // per slot: [0] h2d start, [1] h2d end, [2] compute start, [3] compute end, [4] d2h start, [5] d2h end
   std::vector<hipEvent_t> ev;
   float* d_delays = nullptr;
-  float* h_delays = nullptr;  // pinned staging
   float* d_gains = nullptr;
-  float* h_gains = nullptr;
-  hipEvent_t ev_delays = nullptr, ev_gains = nullptr;
+  // pinned staging rings for control updates: update u uses stage u % kStage, whose previous upload must have
+  // retired (its event) -- so only kStage updates in flight at once can make the caller wait
+  float* h_delays[kStage] = {};
+  float* h_gains[kStage] = {};
+  hipEvent_t ev_delays[kStage] = {}, ev_gains[kStage] = {};
+  long long n_delay_updates = 0, n_gain_updates = 0;
   bool delays_set = false, gains_set = false;
   long long next = 0;
 };
@@ -64,12 +70,14 @@ void release(bf_pipeline* p) {
   for (void* x : p->d_in) (void)hipFree(x);
   for (void* x : p->d_out) (void)hipFree(x);
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
-  if (p->ev_delays) (void)hipEventDestroy(p->ev_delays);
-  if (p->ev_gains) (void)hipEventDestroy(p->ev_gains);
+  for (int i = 0; i < kStage; ++i) {
+    if (p->ev_delays[i]) (void)hipEventDestroy(p->ev_delays[i]);
+    if (p->ev_gains[i]) (void)hipEventDestroy(p->ev_gains[i]);
+    if (p->h_delays[i]) (void)hipHostFree(p->h_delays[i]);
+    if (p->h_gains[i]) (void)hipHostFree(p->h_gains[i]);
+  }
   if (p->d_delays) (void)hipFree(p->d_delays);
   if (p->d_gains) (void)hipFree(p->d_gains);
-  if (p->h_delays) (void)hipHostFree(p->h_delays);
-  if (p->h_gains) (void)hipHostFree(p->h_gains);
   if (p->s_h2d) (void)hipStreamDestroy(p->s_h2d);
   if (p->s_comp) (void)hipStreamDestroy(p->s_comp);
   if (p->s_d2h) (void)hipStreamDestroy(p->s_d2h);
@@ -124,14 +132,18 @@ int bf_pipeline_create(bf_pipeline** out, int B, int C, int T, int A, int M, int
   }
   for (auto& ev : p->ev)
     if ((e = hipEventCreate(&ev)) != hipSuccess) return fail(e, "hipEventCreate");
-  if ((e = hipEventCreateWithFlags(&p->ev_delays, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
-  if ((e = hipEventCreateWithFlags(&p->ev_gains, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+  for (int i = 0; i < kStage; ++i) {
+    if ((e = hipEventCreateWithFlags(&p->ev_delays[i], hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+    if ((e = hipEventCreateWithFlags(&p->ev_gains[i], hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&p->h_delays[i]), p->delay_bytes, hipHostMallocDefault)) !=
+        hipSuccess)
+      return fail(e, "hipHostMalloc");
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&p->h_gains[i]), p->gain_bytes, hipHostMallocDefault)) !=
+        hipSuccess)
+      return fail(e, "hipHostMalloc");
+  }
   if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_delays), p->delay_bytes)) != hipSuccess) return fail(e, "malloc");
   if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_gains), p->gain_bytes)) != hipSuccess) return fail(e, "malloc");
-  if ((e = hipHostMalloc(reinterpret_cast<void**>(&p->h_delays), p->delay_bytes, hipHostMallocDefault)) != hipSuccess)
-    return fail(e, "hipHostMalloc");
-  if ((e = hipHostMalloc(reinterpret_cast<void**>(&p->h_gains), p->gain_bytes, hipHostMallocDefault)) != hipSuccess)
-    return fail(e, "hipHostMalloc");
   *out = p;
   bf::clear_error();
   return BF_OK;
@@ -152,19 +164,24 @@ int bf_pipeline_frame_bytes(const bf_pipeline* p, size_t* in_bytes, size_t* out_
 }
 
 // Stage a host table through pinned memory and upload it on the compute stream (after every frame already
-// submitted, before every later one).  The staging buffer is reused once its previous upload has retired.
-static int upload(bf_pipeline* p, const float* host, float* staging, float* dev, size_t bytes, hipEvent_t done) {
-  BF_HIP(hipEventSynchronize(done));
-  std::memcpy(staging, host, bytes);
-  BF_HIP(hipMemcpyAsync(dev, staging, bytes, hipMemcpyHostToDevice, p->s_comp));
-  BF_HIP(hipEventRecord(done, p->s_comp));
+// submitted, before every later one).  Update u uses staging buffer u % kStage; the caller waits only when that
+// buffer's previous upload (kStage updates ago) is still queued behind in-flight frames.
+static int upload(bf_pipeline* p, const float* host, float* const (&staging)[kStage], float* dev, size_t bytes,
+                  hipEvent_t (&done)[kStage], long long* count) {
+  const int i = static_cast<int>(*count % kStage);
+  BF_HIP(hipEventSynchronize(done[i]));
+  std::memcpy(staging[i], host, bytes);
+  BF_HIP(hipMemcpyAsync(dev, staging[i], bytes, hipMemcpyHostToDevice, p->s_comp));
+  BF_HIP(hipEventRecord(done[i], p->s_comp));
+  ++*count;
   return BF_OK;
 }
 
 int bf_pipeline_set_delays(bf_pipeline* p, const float* host_delay_vals) {
   BF_REQUIRE(p != nullptr && host_delay_vals != nullptr, "bf_pipeline_set_delays: null pointer");
   BF_GUARD(p);
-  const int st = upload(p, host_delay_vals, p->h_delays, p->d_delays, p->delay_bytes, p->ev_delays);
+  const int st = upload(p, host_delay_vals, p->h_delays, p->d_delays, p->delay_bytes, p->ev_delays,
+                        &p->n_delay_updates);
   if (st == BF_OK) p->delays_set = true;
   return st;
 }
@@ -172,12 +189,12 @@ int bf_pipeline_set_delays(bf_pipeline* p, const float* host_delay_vals) {
 int bf_pipeline_set_gains(bf_pipeline* p, const float* host_gains) {
   BF_REQUIRE(p != nullptr, "bf_pipeline_set_gains: null pipeline");
   BF_GUARD(p);
-  if (!host_gains) {  // back to unit weights (stream-ordered like an upload)
-    BF_HIP(hipEventSynchronize(p->ev_gains));
+  if (!host_gains) {  // back to unit weights: frames submitted from now on do not read the gain table
     p->gains_set = false;
+    bf::clear_error();
     return BF_OK;
   }
-  const int st = upload(p, host_gains, p->h_gains, p->d_gains, p->gain_bytes, p->ev_gains);
+  const int st = upload(p, host_gains, p->h_gains, p->d_gains, p->gain_bytes, p->ev_gains, &p->n_gain_updates);
   if (st == BF_OK) p->gains_set = true;
   return st;
 }

@@ -66,6 +66,40 @@ def test_stream_int8_bit_exact_with_updates(context, A, M, C, T, B, depth, signe
         assert sb.done(tickets[-1]) and sb.done(tickets[-1], "input")
 
 
+def test_stream_update_before_every_frame(context):
+    """A new delay model and new beam weights before every frame (more updates in flight than the pipeline's 4
+    staging buffers per table): each frame still uses exactly the model current when it was submitted."""
+    A, M, C, T, B, depth = 19, 3, 5, 64, 2, 3
+    Ctot, bdt = 64 * C, T * 2 * 64 * C * TS
+    tmpl = StreamingBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=0, delay_channels=1, out_int8=True,
+                                       out_scale=1 / 32, t0=0.0, batch_dt=bdt, beam_weights=True, depth=depth)
+    rng = np.random.default_rng(7)
+    n_frames = 4 * depth + 2
+    frames = [rng.integers(0, 256, tmpl.input_shape, dtype=np.uint8) for _ in range(n_frames)]
+    models = []
+    g = np.ones((M, A), np.float32)
+    with tmpl.instantiate() as sb:
+        bufs = sb.host_frames()
+        tickets = []
+        for k, f in enumerate(frames):
+            d = delays(M, A, 100 + k)
+            sb.set_delays(d)
+            w = rng.uniform(-1.5, 1.5, A).astype(np.float32)
+            sb.set_beam_weights(k % M, *w)
+            g = g.copy()
+            g[k % M] = w
+            samples, beams = bufs[k % depth]
+            if k >= depth:
+                sb.wait(tickets[k - depth])
+                check(tickets[k - depth], bufs, depth, frames, models, tmpl, False)
+            samples[...] = f
+            tickets.append(sb.submit(samples, beams))
+            models.append((d, g, tmpl.t0 + k * tmpl.frame_dt))
+        for tk in tickets[-depth:]:
+            sb.wait(tk)
+            check(tk, bufs, depth, frames, models, tmpl, False)
+
+
 def check(ticket, bufs, depth, frames, models, tmpl, signed):
     d, g, t0 = models[ticket]
     ref = O.fused_beamform_int8(frames[ticket], d, tmpl.n_channels, xeng_id=tmpl.xeng_id, t0=t0,
