@@ -293,6 +293,11 @@ __device__ __forceinline__ void store_pol(const FusedArgs& P, int b, int c, int 
   }
 }
 
+// int8 beams requantised from the float accumulators of a full slab, stored as whole rows (defined below).
+template <int NTS>
+__device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, int tau0, int tq, int h, int lane,
+                                     int wave, bool tv, const f32x4 (&acc)[4][NTS]);
+
 // ---------------------------------------------------------------------------------------------------------
 // Persistent, software-pipelined kernel (A <= 64, T <= 256: one load group, one 64-sample chunk per wave).
 // grid = resident workgroups (2 per CU); workgroup g walks items g, g + grid, ... (item = (slab, b, c), c
@@ -364,7 +369,10 @@ __global__ __launch_bounds__(kThreads, 2) void beamform_fused_pipe_kernel(FusedA
           for (int tau = 0; tau < NTS; ++tau) sum += acc[i][tau][0] + acc[i][tau][1] + acc[i][tau][2] + acc[i][tau][3];
         if (sum == 1234.5f) reinterpret_cast<float*>(P.y)[tid] = sum;  // keeps the work alive
       } else {
-        if (tv) store_pol<OutI8, NTS, Full>(P, b, c, p, tau0, nts, tq, h, acc);
+        if constexpr (OutI8 && Full)
+          store_f32acc_i8_rows<NTS>(P, b, c, p, tau0, tq, h, lane, wave, tv, acc);
+        else if (tv)
+          store_pol<OutI8, NTS, Full>(P, b, c, p, tau0, nts, tq, h, acc);
       }
     }
   };
@@ -476,7 +484,10 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_item_kernel(Fuse
         for (int tau = 0; tau < NTS; ++tau) sum += acc[i][tau][0] + acc[i][tau][1] + acc[i][tau][2] + acc[i][tau][3];
       if (sum == 1234.5f) reinterpret_cast<float*>(P.y)[tid] = sum;
     } else {
-      if (tv) store_pol<OutI8, NTS, Full, (Mode & kNtStore) != 0>(P, b, c, p, tau0, nts, tq, h, acc);
+      if constexpr (OutI8 && Full)
+        store_f32acc_i8_rows<NTS>(P, b, c, p, tau0, tq, h, lane, wave, tv, acc);
+      else if (tv)
+        store_pol<OutI8, NTS, Full, (Mode & kNtStore) != 0>(P, b, c, p, tau0, nts, tq, h, acc);
     }
   }
 }
@@ -889,6 +900,45 @@ __device__ __forceinline__ void i8_store_block(const uint32_t (&pk)[NTS][4], int
       }
     }
     if (r < rows) st_i8<Mode>(u32x4_t{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4_t*>(block + 16 * lane + 1024 * si));
+  }
+}
+
+// Float accumulators -> int8 beams (requantise(y, scale) = clamp(rint(RN(y * scale)), +-127), as q8) for a full
+// slab: the magic-number requantisation of the integer path (requant_bits on RN(y * scale)), 4 bytes per v_perm
+// pack, the 4x4 row transpose, then whole-row stores -- 1 KiB ds_bpermute blocks when the slab is the whole row --
+// instead of one 4-byte store per (sample, tile) (the int8 item kernel's store path, 4x fewer, wider stores).
+// Every lane of the wave must be here (permlane / bpermute); `tv` guards only the stores.
+template <int NTS>
+__device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, int tau0, int tq, int h, int lane,
+                                     int wave, bool tv, const f32x4 (&acc)[4][NTS]) {
+  constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
+  const float s = P.out_scale;
+  const int M2 = 2 * P.M;
+  uint32_t pk[NTS][4];
+#pragma unroll
+  for (int tau = 0; tau < NTS; ++tau) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t q[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = __fadd_rn(__fmul_rn(acc[i][tau][r], s), kMagic);
+        q[r] = __float_as_uint(__builtin_amdgcn_fmed3f(v, kMagic - 127.0f, kMagic + 127.0f));
+      }
+      pk[tau][i] = pack_low_bytes(q[0], q[1], q[2], q[3]);
+    }
+    transpose_rows4(pk[tau]);
+  }
+  const size_t prow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T);
+  if (M2 == 16 * NTS) {
+    i8_store_block<NTS, 0>(pk, reinterpret_cast<int8_t*>(P.y) + (prow + 64 * wave) * M2, lane, P.T - 64 * wave);
+    return;
+  }
+  if (tv) {
+    int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 4 * tq + h) * M2 + 16 * tau0;
+#pragma unroll
+    for (int tau = 0; tau < NTS; ++tau)
+      st_i8<0>(u32x4_t{pk[tau][0], pk[tau][1], pk[tau][2], pk[tau][3]}, reinterpret_cast<u32x4_t*>(o + 16 * tau));
   }
 }
 

@@ -602,7 +602,11 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
               int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 2 * tq + i) * M2 + 2 * m0 + 16 * h;
-              *reinterpret_cast<u32x4_t*>(o) = u32x4_t{pk[i][0], pk[i][1], pk[i][2], pk[i][3]};
+              if constexpr ((Mode & 16) != 0)  // diagnostics: non-temporal stores
+                __builtin_nontemporal_store(u32x4_t{pk[i][0], pk[i][1], pk[i][2], pk[i][3]},
+                                            reinterpret_cast<u32x4_t*>(o));
+              else
+                *reinterpret_cast<u32x4_t*>(o) = u32x4_t{pk[i][0], pk[i][1], pk[i][2], pk[i][3]};
             }
           }
         } else if (tq < T2) {  // partial slab / unaligned rows: byte stores with the beam guard
@@ -716,6 +720,8 @@ extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y
     case 1008: return bf::launch_w32<true, 8>(P, st);
     case 1009: return bf::launch_w32<true, 9>(P, st);
     case 1013: return bf::launch_w32<true, 13>(P, st);
+    case 1016: return bf::launch_w32<true, 16>(P, st);
+    case 1017: return bf::launch_w32<true, 17>(P, st);
     default: return BF_ERR_ARG;
   }
 }

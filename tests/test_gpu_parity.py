@@ -370,9 +370,12 @@ def test_item_kernels_workgroup_order(context, command_queue, order, B, C, M):
                           O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, batch_dt=bdt), signed=True)
 
 
-def test_fused_int8_float_path_is_requantised_f32(context, command_queue):
-    """int8_contract='f32' (BF_FUSED_INT8_VIA_F32): float beams requantised in-kernel == bf_requant(float beams)."""
-    B, A, M, C, T, Ctot = 2, 64, 16, 4, 256, 4096
+@pytest.mark.parametrize("A,M,T", [(64, 16, 256), (64, 8, 256), (40, 32, 64), (64, 16, 48), (33, 24, 128),
+                                   (64, 1, 256)])
+def test_fused_int8_float_path_is_requantised_f32(context, command_queue, A, M, T):
+    """int8_contract='f32' (BF_FUSED_INT8_VIA_F32): float beams requantised in-kernel == bf_requant(float beams).
+    Shapes: whole-row slabs (1 KiB store blocks), multi-slab rows, partial waves (T < 256), partial tiles, 1 beam."""
+    B, C, Ctot = 2, 4, 4096
     d = random_delays(1, M, A, 9)
     raw = O.u8_voltages((B, A, C, T, 2, 2), seed=9).view(np.int8)
     scale = 1.0 / 64

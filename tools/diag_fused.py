@@ -59,9 +59,11 @@ ROUNDS = int(_os.environ.get("DIAG_ROUNDS", "1"))
 if "wide" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_wide.argtypes = [I, I, V, V, V, I, I, I, I, I, I, D, V]
     wnames = {0: "full (fast coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 3: "no-coef,no-mfma",
-              5: "no-coef,no-store"}
+              5: "no-coef,no-store", 16: "nt stores"}
+    if _os.environ.get("WIDE_MODES"):
+        wnames = {int(m): wnames.get(int(m), str(m)) for m in _os.environ["WIDE_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
-    for tw in (2, 1):
+    for tw in [int(t) for t in _os.environ.get("WIDE_TW", "2,1").split(",")]:
         res = {m: [] for m in wnames}
         for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
             for mode in wnames:
@@ -80,7 +82,8 @@ if "w8" in _os.environ.get("DIAG_KERNELS", ""):
                83: "16 rows,slab0,no-coef,no-mfma", 259: "xcd-range,no-coef,no-mfma", 275: "xcd-range,slab0,nc,nm",
                256: "xcd-range (full)", 512: "branchy phasors (old)",
                1000: "w32 full", 1001: "w32 no-coef", 1002: "w32 no-mfma", 1003: "w32 no-coef,no-mfma",
-               1004: "w32 no-store", 1008: "w32 no-load", 1009: "w32 no-coef,no-load", 1013: "w32 nc,nl,ns"}
+               1004: "w32 no-store", 1008: "w32 no-load", 1009: "w32 no-coef,no-load", 1013: "w32 nc,nl,ns",
+               1016: "w32 nt stores", 1017: "w32 nt stores, no-coef"}
     if _os.environ.get("W8_MODES"):
         w8names = {int(m): w8names.get(int(m), str(m)) for m in _os.environ["W8_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
