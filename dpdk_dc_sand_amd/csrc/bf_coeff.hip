@@ -40,6 +40,51 @@ __global__ __launch_bounds__(256) void coeff_gen_kernel(const float4* __restrict
   }
 }
 
+// Tiled form (32 antennas x 32 beams per workgroup): the delay model is [c][m][a] (antenna fastest) and the table
+// [c][2a][2m] (beam fastest), so the one-thread-per-(a, m) kernel above reads the model with a 4 KiB lane stride at
+// 256 antennas (a 64-byte line per 16-byte entry: 4x over-fetch of a 1 GiB model at config 4).  Here the tile's
+// model rows are read coalesced (antenna fastest) into LDS, and each thread then takes its entries beam-fastest
+// for the phasor and the coalesced table stores.
+constexpr int kCoefTile = 32;
+__global__ __launch_bounds__(256) void coeff_gen_tile_kernel(const float4* __restrict__ dv, float* __restrict__ out,
+                                                             int B, int P, int C, int A, int M, long long base_ch,
+                                                             double ctot, double ts) {
+  __shared__ float4 tile[kCoefTile][kCoefTile + 1];  // [a][m], padded row
+  const int c = static_cast<int>(blockIdx.y);
+  const int ntm = (M + kCoefTile - 1) / kCoefTile;
+  const int a0 = static_cast<int>(blockIdx.x) / ntm * kCoefTile, m0 = static_cast<int>(blockIdx.x) % ntm * kCoefTile;
+  const int t = static_cast<int>(threadIdx.x);
+  {
+    const int la = t & 31;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int lm = (t >> 5) + 8 * j;
+      const int a = min(a0 + la, A - 1), m = min(m0 + lm, M - 1);
+      tile[la][lm] = dv[(static_cast<size_t>(c) * M + m) * A + a];  // delay_vals[c][m][a]
+    }
+  }
+  __syncthreads();
+  const int lm = t & 31, m = m0 + lm;
+  const size_t plane = static_cast<size_t>(2 * A) * (2 * M);  // one (b, p, c) coefficient matrix
+  const size_t bp_stride = static_cast<size_t>(C) * plane;
+  const PhaseK k = make_phase(ctot, ts);
+  const double ch = static_cast<double>(base_ch + c);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int la = (t >> 5) + 8 * j, a = a0 + la;
+    if (a >= A || m >= M) continue;
+    float re, im;
+    steering_coeff(tile[la][lm], ch, k, 0.0, &re, &im);
+    const float2 row0 = make_float2(re, im);   // W[2a][2m], W[2a][2m+1]
+    const float2 row1 = make_float2(-im, re);  // W[2a+1][2m], W[2a+1][2m+1]
+    float* w = out + static_cast<size_t>(c) * plane + static_cast<size_t>(2 * a) * (2 * M) + 2 * m;
+    for (int bp = 0; bp < B * P; ++bp) {
+      *reinterpret_cast<float2*>(w + bp * bp_stride) = row0;
+      *reinterpret_cast<float2*>(w + bp * bp_stride + 2 * M) = row1;
+    }
+  }
+}
+
 template <bool F16>
 __global__ __launch_bounds__(256) void coeff_gen_time_kernel(const float4* __restrict__ dv, int delay_channels,
                                                              void* __restrict__ out, int n_times, int C, int A, int M,
@@ -83,6 +128,14 @@ extern "C" int bf_coeff_gen(const float* delay_vals, float* out, int B, int P, i
   BF_REQUIRE((reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0,
              "bf_coeff_gen: misaligned buffer");
   BF_REQUIRE(static_cast<long long>(A) * M < (1LL << 31) && C < 65536, "bf_coeff_gen: shape too large");
+  if (A >= 32 && M >= 32) {  // many antennas and beams: the tiled, coalesced-read form
+    const unsigned gx = static_cast<unsigned>(((A + bf::kCoefTile - 1) / bf::kCoefTile) *
+                                              ((M + bf::kCoefTile - 1) / bf::kCoefTile));
+    hipLaunchKernelGGL(bf::coeff_gen_tile_kernel, dim3(gx, static_cast<unsigned>(C)), dim3(256), 0,
+                       bf::as_stream(stream), reinterpret_cast<const float4*>(delay_vals), out, B, P, C, A, M,
+                       static_cast<long long>(C) * xeng_id, static_cast<double>(Ctot), sample_period);
+    BF_LAUNCHED("coeff_gen_tile_kernel");
+  }
   const unsigned gx = static_cast<unsigned>((static_cast<long long>(A) * M + 255) / 256);
   hipLaunchKernelGGL(bf::coeff_gen_kernel, dim3(gx, static_cast<unsigned>(C)), dim3(256), 0, bf::as_stream(stream),
                      reinterpret_cast<const float4*>(delay_vals), out, B, P, C, A, M,

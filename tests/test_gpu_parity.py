@@ -128,6 +128,16 @@ def test_beamform_coeffs(context, command_queue, n_batches, n_ants, n_channels, 
     np.testing.assert_array_equal(O.coeffs(d, n_batches, 2, C, n_channels, n_ants, n_beams, xeng_id), w)
 
 
+@pytest.mark.parametrize("A,M,C", [(256, 64, 3), (40, 33, 2), (32, 32, 2), (100, 47, 1), (33, 70, 2)])
+def test_coeff_gen_tiled_matches_oracle(context, command_queue, A, M, C):
+    """The tiled coefficient generator (A >= 32 and M >= 32: 32 x 32 tiles, coalesced model reads through LDS),
+    ragged tiles included: bit-exact to the coefficient contract, random per-(c, m, a) delays."""
+    d = random_delays(C, M, A, A * M)
+    op = CoeffGeneratorTemplate(context, 2, 2, C, 8192, 16, 16, A, M, 3, TS).instantiate(command_queue)
+    (w,) = run(op, command_queue, {"delay_vals": d}, ["outCoeffs"])
+    np.testing.assert_array_equal(O.coeffs(d, 2, 2, C, 8192, A, M, 3), w)
+
+
 def test_coeff_gen_time_matches_oracle(context, command_queue):
     from dpdk_dc_sand_amd import accel
     C, A, M, Ctot, nt = 6, 5, 3, 4096, 4
