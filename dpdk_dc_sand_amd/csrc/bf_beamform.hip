@@ -33,42 +33,43 @@
 namespace bf {
 
 // ---------------------------------------------------------------------------------------------------------
-// Stage W[b,p,c][:, slab columns] (rows k < Sp*32, zero past 2A and past 2M) -> hi/lo fragments in LDS.  Each thread
-// moves 4 consecutive columns of a row per float4 load (2M % 4 == 0; scalar otherwise), and batches of 8 loads are
-// all issued before their conversions: a load-then-convert loop paid one memory latency per element.
+// Stage W[b,p,c][:, slab columns] (rows k < Sp*32, zero past 2A and past 2M) -> hi/lo fragments in LDS.  A thread
+// takes 8 consecutive k of one column (a fragment lane's 8 halves): 8 dword loads down the column (32 threads read
+// 128 contiguous bytes of each row), all issued before any conversion, then one ds_write_b128 per limb.  (Round 1
+// staged float4 rows with a runtime division per element and two 2-byte LDS writes per value: at 256 antennas the
+// staging alone cost ~540 us of a 2 ms launch.)
 template <int NTS>
 __device__ __forceinline__ void stage_table(_Float16* lh, const float* __restrict__ wp, int K2, int M2, int Sp,
                                             int tau0, int nts, int tid) {
-  const int cols = nts * 16, c4 = cols >> 2;
-  const int n4 = Sp * 32 * c4;
-  const bool vec = (M2 & 3) == 0 && (reinterpret_cast<uintptr_t>(wp) & 15) == 0;  // 16-byte rows (uniform)
-  for (int base = 0; base < n4; base += 8 * kThreads) {
-    float4 v[8];
+  constexpr int cols = NTS * 16;
+  const int npairs = Sp * 4 * cols;  // (k block of 8, column)
+  for (int e0 = 0; e0 < npairs; e0 += 2 * kThreads) {
+    float v[2][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = min(base + j * kThreads + tid, n4 - 1);
-      const int k = e / c4, cl = (e - k * c4) * 4;
-      const int col = tau0 * 16 + cl;
-      const int kk = min(k, K2 - 1);
-      if (vec) {
-        v[j] = *reinterpret_cast<const float4*>(wp + static_cast<size_t>(kk) * M2 + min(col, M2 - 4));
-      } else {
-        const float* r = wp + static_cast<size_t>(kk) * M2;
-        v[j] = float4{r[min(col, M2 - 1)], r[min(col + 1, M2 - 1)], r[min(col + 2, M2 - 1)], r[min(col + 3, M2 - 1)]};
-      }
+    for (int u = 0; u < 2; ++u) {
+      const int e = min(e0 + u * kThreads + tid, npairs - 1);
+      const int kb = e / cols, cl = e % cols;  // cols is a power of two: shifts
+      const int col = min(tau0 * 16 + cl, M2 - 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[u][j] = wp[static_cast<size_t>(min(8 * kb + j, K2 - 1)) * M2 + col];
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = base + j * kThreads + tid;
-      if (e >= n4) break;
-      const int k = e / c4, cl = (e - k * c4) * 4;
-      const int col = tau0 * 16 + cl;
-      const float vals[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+    for (int u = 0; u < 2; ++u) {
+      const int e = e0 + u * kThreads + tid;
+      if (e >= npairs) break;
+      const int kb = e / cols, cl = e % cols;
+      if (cl >= 16 * nts) continue;  // past the slab's last tile (partial slab)
+      const bool colok = tau0 * 16 + cl < M2;
+      half8 hi, lo;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float val = (k < K2 && col + q < M2) ? vals[q] : 0.0f;
-        put_split(lh, coef_elem(k, cl + q, nts), val);
+      for (int j = 0; j < 8; ++j) {
+        const float w = (colok && 8 * kb + j < K2) ? v[u][j] : 0.0f;
+        hi[j] = static_cast<_Float16>(w);
+        lo[j] = static_cast<_Float16>(w - static_cast<float>(hi[j]));  // exact difference, then rounded
       }
+      const int e8 = coef_elem(8 * kb, cl, nts);  // 8 consecutive halves of one lane's fragment
+      *reinterpret_cast<half8*>(lh + e8) = hi;
+      *reinterpret_cast<half8*>(lh + e8 + 64 * 8) = lo;
     }
   }
 }
@@ -162,11 +163,11 @@ __global__ __launch_bounds__(kThreads) void beamform_table_kernel(const uint8_t*
 }
 
 // Streaming variant for A % 4 == 0 (8-byte fragment loads): a wave's k-step fragments of all its row groups form one
-// stream that runs through a register ring of R uint2, refilled R steps ahead by unconditional loads (address clamped
-// inside the table; steps past S meet zero coefficients).  The loop body is identical every iteration, so the
-// compiler's vmcnt waits stay exact (vmcnt(R-1) per step) and R loads stay in flight -- the per-step load-then-use of
+// stream that runs through a register ring of R steps x G row groups, refilled R steps ahead by unconditional loads
+// (address clamped inside the table; steps past S meet zero coefficients).  The loop body is identical every
+// iteration, so the compiler's vmcnt waits stay exact and R G loads stay in flight -- the per-step load-then-use of
 // the basic kernel paid one memory latency per k-step (32 per row at 256 antennas).
-template <bool Signed, int NTS, int R>
+template <bool Signed, int NTS, int R, int Mode = 0>
 __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uint8_t* __restrict__ x,
                                                                        const float* __restrict__ w,
                                                                        float* __restrict__ y, int NB, int A, int M,
@@ -187,54 +188,98 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
   float* yp = y + bpc * static_cast<size_t>(T) * M2;
   const int h = lane >> 4, tl = lane & 15;
   const int nrg = (NB - wave + kWaves - 1) / kWaves;  // this wave's row groups (rg = wave + 4 j)
-  const int nsteps = max(nrg, 1) * Sp;  // the wave's whole fragment stream (a wave without rows streams row 0)
-  // stream position q -> (row group j = q / Sp, step s = q % Sp); byte offset of the lane's 8 bytes, clamped
-  auto src = [&](int q) -> const uint2* {
-    q = min(q, nsteps - 1);
-    const int j = q / Sp, s = q - j * Sp;
-    const int tt = min((wave + kWaves * j) * kSamplesPerBlock + tl, T - 1);  // in the item even for row-less waves
-    const int k0 = min(32 * s + 8 * h, K2 - 8);
-    return reinterpret_cast<const uint2*>(xp + static_cast<size_t>(tt) * K2 + k0);
+  // G row groups are contracted together (each LDS table fragment feeds G x 2 MFMAs, 2 G NTS accumulator chains);
+  // the lane's row pointer of row group j is computed once per row group (round 1 recomputed a division and a
+  // 64-bit product per load: ~1.3 ms of a 2 ms launch went to streaming x at 256 antennas)
+  constexpr int G = 2;
+  auto rowp = [&](int j) -> const uint8_t* {  // clamped inside the item even for row-less waves
+    return xp + static_cast<size_t>(min((wave + kWaves * j) * kSamplesPerBlock + tl, T - 1)) * K2;
   };
-  // the ring's first R fragments are requested BEFORE the coefficient table: vmcnt counts in order, so the table
-  // conversion's wait then covers both, and the voltage latency overlaps the table's
-  uint2 ring[R];
+  // (a 16-byte, two-step load per lane would permute the k summation order, and the fused kernels' bitwise
+  // equality with this chain rests on the same order: 8-byte, one-step loads)
+  const int kh = 8 * h;
+  auto ld = [&](const uint8_t* row, int s) -> uint2 {
+    if constexpr (Mode & 8) return uint2{static_cast<uint32_t>(s + tl), static_cast<uint32_t>(s)};
+    return *reinterpret_cast<const uint2*>(row + min(32 * s + kh, K2 - 8));
+  };
+  const uint8_t* cur_rows[G];
+  const uint8_t* next_rows[G];
 #pragma unroll
-  for (int r = 0; r < R; ++r) ring[r] = *src(r);
+  for (int g = 0; g < G; ++g) {
+    cur_rows[g] = rowp(g);
+    next_rows[g] = rowp(G + g);
+  }
+  // the ring's first R steps are requested BEFORE the coefficient table: vmcnt counts in order, so the table
+  // conversion's wait then covers both, and the voltage latency overlaps the table's
+  uint2 ring[R][G];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int g = 0; g < G; ++g) ring[r][g] = ld(cur_rows[g], r);
   __builtin_amdgcn_sched_barrier(0);
-  stage_table<NTS>(reinterpret_cast<_Float16*>(lds), w + bpc * static_cast<size_t>(K2) * M2, K2, M2, Sp, tau0, nts,
-                   tid);  // padded steps zero
+  // Mode (diagnostics only): 1 no table staging, 2 no MFMA, 4 no stores, 8 no voltage loads
+  if constexpr (!(Mode & 1))
+    stage_table<NTS>(reinterpret_cast<_Float16*>(lds), w + bpc * static_cast<size_t>(K2) * M2, K2, M2, Sp, tau0, nts,
+                     tid);  // padded steps zero
   __syncthreads();
   if (nrg <= 0) return;
 
-  f32x4 acc[NTS];
+  const int npair = (nrg + G - 1) / G;
+  for (int pi = 0; pi < npair; ++pi) {
+    f32x4 acc[G][NTS];
 #pragma unroll
-  for (int tau = 0; tau < NTS; ++tau) acc[tau] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int q0 = 0; q0 < nsteps; q0 += R) {
-    const int j = q0 / Sp, s0 = q0 - j * Sp;  // R divides Sp: a ring turn stays inside one row group
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint2 cur = ring[r];
-      ring[r] = *src(q0 + R + r);
-      const int s = s0 + r;
-      const half8 v = bytes8_to_frag<Signed>(cur.x, cur.y);
+      for (int tau = 0; tau < NTS; ++tau) acc[g][tau] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < Sp; s0 += R) {  // R divides Sp
+      const bool nx = s0 + R >= Sp;      // this ring turn prefetches the next row groups' first steps
+      const int sb = nx ? 0 : s0 + R;
 #pragma unroll
-      for (int tau = 0; tau < NTS; ++tau) {
-        if (tau < nts) {
-          const int slot = ((s * nts + tau) * 2) * 64;
-          acc[tau] = mfma(lds[slot + lane], v, acc[tau]);
-          acc[tau] = mfma(lds[slot + 64 + lane], v, acc[tau]);
+      for (int r = 0; r < R; ++r) {
+        half8 v[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const uint2 cur = ring[r][g];
+          ring[r][g] = ld(nx ? next_rows[g] : cur_rows[g], sb + r);
+          v[g] = bytes8_to_frag<Signed>(cur.x, cur.y);
+        }
+        const int s = s0 + r;
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau) {
+          if (tau < nts) {
+            const int slot = ((s * nts + tau) * 2) * 64;
+            const half8 chi = lds[slot + lane], clo = lds[slot + 64 + lane];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+              if constexpr (Mode & 2) {
+                acc[g][tau] += __builtin_bit_cast(f32x4, v[g]) + __builtin_bit_cast(f32x4, chi);
+              } else {
+                acc[g][tau] = mfma(chi, v[g], acc[g][tau]);
+                acc[g][tau] = mfma(clo, v[g], acc[g][tau]);
+              }
+            }
+          }
         }
       }
     }
-    if (s0 + R == Sp) {  // row group j complete: store and restart the accumulators
-      const int tt = (wave + kWaves * j) * kSamplesPerBlock + tl;
-      float* orow = yp + static_cast<size_t>(tt) * M2;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int j = pi * G + g;
+      if (j >= nrg) break;
+      float* orow = yp + static_cast<size_t>((wave + kWaves * j) * kSamplesPerBlock + tl) * M2;
 #pragma unroll
       for (int tau = 0; tau < NTS; ++tau) {
-        if (tau < nts) store_f32<NTS>(orow, 16 * (tau0 + tau) + 4 * h, M2, acc[tau]);
-        acc[tau] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (Mode & 4) {
+          if (acc[g][tau][0] == 1234.5f) orow[tau] = acc[g][tau][1];
+        } else {
+          if (tau < nts) store_f32<NTS>(orow, 16 * (tau0 + tau) + 4 * h, M2, acc[g][tau]);
+        }
       }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      cur_rows[g] = next_rows[g];
+      next_rows[g] = rowp((pi + 2) * G + g);
     }
   }
 }
@@ -253,7 +298,7 @@ int launch_table(const uint8_t* x, const float* w, float* y, long long bpc, int 
   BF_LAUNCHED("beamform_table_kernel");
 }
 
-template <bool Signed, int NTS, int R>
+template <bool Signed, int NTS, int R, int Mode = 0>
 int launch_ring(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                 hipStream_t st) {
   const int nslabs = (NT + NTS - 1) / NTS;
@@ -263,7 +308,8 @@ int launch_ring(const uint8_t* x, const float* w, float* y, long long bpc, int N
   const int xcd = nslabs > 1;
   const long long grid = xcd ? (bpc + 7) / 8 * 8 * nslabs : bpc * nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform: grid too large");
-  hipLaunchKernelGGL((beamform_table_ring_kernel<Signed, NTS, R>), dim3(static_cast<unsigned>(grid)), dim3(kThreads),
+  hipLaunchKernelGGL((beamform_table_ring_kernel<Signed, NTS, R, Mode>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kThreads),
                      lds, st, x, w, y, NB, A, M, S, NT, nslabs, bpc, xcd);
   BF_LAUNCHED("beamform_table_ring_kernel");
 }
@@ -324,3 +370,30 @@ extern "C" int bf_beamform(const uint8_t* x, const float* w, float* y, int B, in
   if (sample_signed) return bf::dispatch_table<true>(x, w, y, bpc, NB, A, M, S, NT, st);
   return bf::dispatch_table<false>(x, w, y, bpc, NB, A, M, S, NT, st);
 }
+
+#ifdef BF_DIAG
+// Diagnostics: ablation of the MatrixMultiply ring kernel at a 256-antenna shape (tools/diag_fused.py,
+// DIAG_KERNELS=table): NTS 2 (two workgroups per CU) or 4 (one), R = 16; mode = the kernel's Mode bits.
+extern "C" int bf_diag_table(int mode, int nts, const uint8_t* x, const float* w, float* y, int B, int P, int C,
+                             int NB, int A, int M, void* stream) {
+  const int S = (2 * A + 31) / 32, NT = (2 * M + 15) / 16;
+  const long long bpc = static_cast<long long>(B) * P * C;
+  hipStream_t st = bf::as_stream(stream);
+#define BF_TABLE_MODE(m)                                                                                      \
+  case m:                                                                                                     \
+    return nts == 4 ? bf::launch_ring<true, 4, 16, m>(x, w, y, bpc, NB, A, M, S, NT, st)                      \
+                    : bf::launch_ring<true, 2, 16, m>(x, w, y, bpc, NB, A, M, S, NT, st)
+  switch (mode) {
+    BF_TABLE_MODE(0);
+    BF_TABLE_MODE(1);
+    BF_TABLE_MODE(2);
+    BF_TABLE_MODE(4);
+    BF_TABLE_MODE(8);
+    BF_TABLE_MODE(9);
+    BF_TABLE_MODE(6);
+    BF_TABLE_MODE(7);
+    default: return BF_ERR_ARG;
+  }
+#undef BF_TABLE_MODE
+}
+#endif

@@ -192,3 +192,16 @@ if _os.environ.get("DIAG_ITEMREAD"):  # the wide kernels' item-major read patter
                 t = timeit(lambda i: lib.bf_diag_item_read(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, A, C, R, grid,
                                                            10 * pat + ui, q.handle))
                 print(f"  item-read {pname:20s} grid {grid:5d} U {u:2d} {t*1e6:8.1f} us  {nin/t/1e9:7.1f} GB/s")
+if "table" in _os.environ.get("DIAG_KERNELS", ""):  # the MatrixMultiply drop-in's ring kernel at 256 ants x 64 beams
+    lib.bf_diag_table.argtypes = [I, I, V, V, V, I, I, I, I, I, I, V]
+    tnames = {0: "full", 1: "no table staging", 2: "no-mfma", 4: "no-store", 8: "no x loads", 9: "no staging, no x",
+              6: "no-mfma,no-store", 7: "staging+x loads only? (no mfma/store, no staging)"}
+    xb = accel.DeviceArray(ctx, (B * 2 * C * T * A * 2,), np.uint8)
+    wt = accel.DeviceArray(ctx, (B * 2 * C * 2 * A * 2 * M,), np.float32)
+    yt = accel.DeviceArray(ctx, (B * 2 * C * T * 2 * M,), np.float32)
+    _lib.call("bf_memset", wt.ptr, 0, wt.nbytes if hasattr(wt, "nbytes") else B * 2 * C * 2 * A * 2 * M * 4, q.handle)
+    tb = 2 * B * 2 * C * T * A + B * 2 * C * 2 * A * 2 * M * 4 + B * 2 * C * T * 2 * M * 4
+    for nts in (2, 4):
+        for mode, nm in tnames.items():
+            t = timeit(lambda i: lib.bf_diag_table(mode, nts, xb.ptr, wt.ptr, yt.ptr, B, 2, C, T // 16, A, M, q.handle))
+            print(f"  table nts={nts} mode {mode:2d} {nm:26s} {t*1e6:8.1f} us  alg {tb/t/1e9:7.1f} GB/s")
