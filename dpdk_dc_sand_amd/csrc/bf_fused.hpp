@@ -76,6 +76,16 @@ __device__ __forceinline__ void transpose_rows4(uint32_t (&v)[4]) {
   v[3] = d[1];
 }
 
+// Workgroup barrier for LDS hand-over only: waits for this wave's LDS operations (lgkmcnt(0)), not its global
+// loads.  __syncthreads() also drains vmcnt, so a voltage prefetch issued before the coefficient phase would have
+// to land before the barrier and the contraction would start with nothing in flight.
+__device__ __forceinline__ void lds_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0); vmcnt and expcnt at their maxima (no wait)
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 // Kernel-path override of a launch (flags & BF_FUSED_PATH_MASK): 0 automatic, else one of the BF_FUSED_PATH_* values.
 inline int fused_kernel_choice(const FusedArgs& P) { return P.path; }
 

@@ -423,7 +423,7 @@ __device__ __forceinline__ void w32_mfma(const int4* __restrict__ fr, int s, int
 }
 
 // Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads.
-template <bool Signed, int Mode = 0>
+template <bool Signed, int Mode = 0, bool Gain = false>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -462,41 +462,70 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
       lchunk += 4;
     }
   };
+  // Q14 limbs of the slab's [[R, I], [-I, R]] blocks (as the 16-beam kernel), under the voltage loads.  Pair e -> 4
+  // consecutive slot antennas x beam row ml = (tid >> 2) % 32, slot antenna sa0 + 8 J.  The first batch's delay
+  // model is requested BEFORE the voltage prefetch (vmcnt counts in order: loaded after it, the first batch waited
+  // for all 32 voltage loads before its phasors could start).
+  const int ml = (tid >> 2) & (kW32Beams - 1);
+  const int sa0 = 4 * (tid >> 7) + (tid & 3);
+  const bool m_ok = m0 + ml < P.M;
+  const float4* dv_row =
+      P.dv + (static_cast<size_t>(P.delay_channels == 1 ? 0 : c) * P.M + min(m0 + ml, P.M - 1)) * P.A;
+  // gains: the launch picks the Gain instantiation, so no branch sits between the loads and their use (a branch
+  // around the gain loads made the compiler wait for every earlier load at the merge)
+  const float* g_row = Gain ? P.gain + static_cast<size_t>(min(m0 + ml, P.M - 1)) * P.A : nullptr;
+  constexpr int kBatch = 8;
+  auto batch_model = [&](int j0, float4 (&dv)[kBatch], float (&gv)[kBatch]) {
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int sa = sa0 + 8 * (j0 + j), st = sa >> 5;
+      const int a = min(w8_step_base(st, P.A) + (sa & 31), P.A - 1);
+      dv[j] = dv_row[a];
+      if constexpr (Gain)
+        gv[j] = g_row[a];
+      else
+        gv[j] = 1.0f;
+    }
+  };
+  float4 dv_first[kBatch];
+  float gv_first[kBatch];
+  if constexpr (!(Mode & 1)) batch_model(0, dv_first, gv_first);
+  __builtin_amdgcn_sched_barrier(0);
+
   uint32_t d0[8][2], d1[8][2], d2[8][2], d3[8][2];
   issue(d0);
   issue(d1);
   issue(d2);
   issue(d3);
+  __builtin_amdgcn_sched_barrier(0);
 
-  // Q14 limbs of the slab's [[R, I], [-I, R]] blocks (as the 16-beam kernel), under the loads.  Pair e -> 4
-  // consecutive slot antennas x beam row ml = (tid >> 2) % 32, slot antenna sa0 + 8 J.
   {
     const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
     const double ch = static_cast<double>(P.base_ch + c);
-    const int cd = P.delay_channels == 1 ? 0 : c;
     const int nj = 4 * Sp;  // 32 Sp slot antennas x 32 beams / 256 threads
     int cs0 = 0, cs1 = 0;
-    const int ml = (tid >> 2) & (kW32Beams - 1);
-    const int sa0 = 4 * (tid >> 7) + (tid & 3);
-    const int m = m0 + ml;
-    const bool m_ok = m < P.M;
-    const float4* dv_row = P.dv + (static_cast<size_t>(cd) * P.M + min(m, P.M - 1)) * P.A;
-    const float* g_row = P.gain ? P.gain + static_cast<size_t>(min(m, P.M - 1)) * P.A : nullptr;
     const int off0 = coef8_byte(2 * sa0, 2 * ml, 4, 0);
-    constexpr int kBatch = 8;
     for (int j0 = 0; j0 < nj; j0 += kBatch) {
       float4 dv[kBatch];
       float gv[kBatch];
       bool valid[kBatch];
       int wc[kBatch], ws[kBatch];
+      if constexpr (!(Mode & 1)) {
+        if (j0 == 0) {
+#pragma unroll
+          for (int j = 0; j < kBatch; ++j) {
+            dv[j] = dv_first[j];
+            gv[j] = gv_first[j];
+          }
+        } else {
+          batch_model(j0, dv, gv);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < kBatch; ++j) {
         const int sa = sa0 + 8 * (j0 + j), st = sa >> 5;
         const int a = w8_step_base(st, P.A) + (sa & 31);
         valid[j] = j0 + j < nj && m_ok && a >= 32 * st;  // rows an earlier step already covered stay zero
-        if constexpr (Mode & 1) continue;
-        dv[j] = dv_row[min(a, P.A - 1)];
-        gv[j] = g_row ? g_row[min(a, P.A - 1)] : 1.0f;
       }
       if constexpr (Mode & 1) {
 #pragma unroll
@@ -533,7 +562,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
       }
     }
   }
-  __syncthreads();
+  lds_barrier();  // the table is complete; the voltage prefetch stays in flight
 
   const float s32 = P.out_scale * 0x1p-14f;
   const int M2 = 2 * P.M;
@@ -637,8 +666,12 @@ int launch_w32(FusedArgs P, hipStream_t st) {
   const long long items = static_cast<long long>(P.B) * P.C;
   const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
-  hipLaunchKernelGGL((beamform_fused_i8_w32_kernel<Signed, Mode>), dim3(static_cast<unsigned>(grid)),
-                     dim3(kW8Threads), lds, st, P);
+  if (P.gain)
+    hipLaunchKernelGGL((beamform_fused_i8_w32_kernel<Signed, Mode, true>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW8Threads), lds, st, P);
+  else
+    hipLaunchKernelGGL((beamform_fused_i8_w32_kernel<Signed, Mode, false>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW8Threads), lds, st, P);
   BF_LAUNCHED("beamform_fused_i8_w32_kernel");
 }
 

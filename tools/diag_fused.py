@@ -59,7 +59,7 @@ ROUNDS = int(_os.environ.get("DIAG_ROUNDS", "1"))
 if "wide" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_wide.argtypes = [I, I, V, V, V, I, I, I, I, I, I, D, V]
     wnames = {0: "full (fast coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 3: "no-coef,no-mfma",
-              5: "no-coef,no-store", 16: "nt stores"}
+              5: "no-coef,no-store", 16: "nt stores", 32: "branchy phasor validity"}
     if _os.environ.get("WIDE_MODES"):
         wnames = {int(m): wnames.get(int(m), str(m)) for m in _os.environ["WIDE_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
