@@ -360,26 +360,25 @@ __host__ __device__ inline size_t w32_lds_bytes(int A) {
 
 // One step's voltages: 8 antennas' 8-byte runs.  (Raw buffer loads with the row offsets as soffsets would save the
 // ~28 VALU of 64-bit address arithmetic per step, but their SGPRs pushed this 247-VGPR kernel into spills.)
+// (kept as 8-byte vectors: split into scalar arrays, the pairs were re-packed into the loop's registers with copies
+// that made the prologue wait for its own prefetch)
 template <int Mode>
 __device__ __forceinline__ void w32_load(const uint8_t* __restrict__ base, size_t ant_stride, uint32_t loff, int s,
-                                         int A, uint32_t (&d)[8][2]) {
+                                         int A, u32x2_t (&d)[8]) {
   const int a0 = w8_step_base(s, A);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     if constexpr (Mode & 8) {
-      d[q][0] = loff * 0x01010101u + s + q;
-      d[q][1] = loff * 0x01010101u + s - q;
+      d[q] = u32x2_t{loff * 0x01010101u + s + q, loff * 0x01010101u + s - q};
       continue;
     }
-    const u32x2_t v = *reinterpret_cast<const u32x2_t*>(base + static_cast<size_t>(a0 + q) * ant_stride + loff);
-    d[q][0] = v[0];
-    d[q][1] = v[1];
+    d[q] = *reinterpret_cast<const u32x2_t*>(base + static_cast<size_t>(a0 + q) * ant_stride + loff);
   }
 }
 
 // The step's B fragments [pol][sample] (one v_perm per dword); the voltage registers are free afterwards.
 template <bool Signed>
-__device__ __forceinline__ void w32_frags(const uint32_t (&d)[8][2], i32x4_t (&f)[2][2]) {
+__device__ __forceinline__ void w32_frags(const u32x2_t (&d)[8], i32x4_t (&f)[2][2]) {
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -387,7 +386,8 @@ __device__ __forceinline__ void w32_frags(const uint32_t (&d)[8][2], i32x4_t (&f
       uint32_t w[4];
 #pragma unroll
       for (int m2 = 0; m2 < 4; ++m2) {
-        uint32_t a = d[2 * m2][i], b = d[2 * m2 + 1][i];
+        const u32x2_t da = d[2 * m2], db = d[2 * m2 + 1];
+        uint32_t a = i ? da.y : da.x, b = i ? db.y : db.x;
         if constexpr (!Signed) {  // x - 128 as int8 (128 * column sum added back at the end)
           a ^= 0x80808080u;
           b ^= 0x80808080u;
@@ -426,6 +426,10 @@ __device__ __forceinline__ void w32_mfma(const int4* __restrict__ fr, int s, int
 template <bool Signed, int Mode = 0, bool Gain = false>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
+  // Mode 128 (diagnostics): per-wave s_memtime cycles of the phases -> P.gain as uint64 [wave][4]: coefficient
+  // phase (to the barrier), contraction loops, requantise + stores, total
+  unsigned long long st_t0 = 0, st_c = 0, st_l = 0, st_s = 0, st_m = 0;
+  if constexpr ((Mode & 128) != 0) st_t0 = __builtin_amdgcn_s_memtime();
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
   int slab, bc;
@@ -451,16 +455,20 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
   int* partial = reinterpret_cast<int*>(lb + static_cast<size_t>(Sp) * 4 * 2 * 64 * 16);  // [4 waves][32 columns]
 
   // the voltage prefetch: step ls of chunk lchunk next; runs on from one chunk into the wave's next one
+  __builtin_assume(Sp >= 4 && (Sp & 3) == 0 && npasses >= 1);  // w32_steps, T >= 2: the 4 priming loads are real
   const int total = npasses * Sp;
   int issued = 0, ls = 0, lchunk = wave;
   // (past the wave's last step it repeats that step: the same, just-fetched bytes, and straight-line code)
-  auto issue = [&](uint32_t (&d)[8][2]) {
+  auto issue = [&](u32x2_t (&d)[8]) {
     const uint32_t loff = hoff + static_cast<uint32_t>(min(lchunk * 16 + tl, T2 - 1)) * 8u;
     w32_load<Mode>(base, ant_stride, loff, ls, P.A, d);
-    if (++issued < total && ++ls == Sp) {
-      ls = 0;
-      lchunk += 4;
-    }
+    // advance with selects, not branches: a branch here made the compiler re-home the step buffers through copies
+    // (and wait for their loads) at the merge
+    ++issued;
+    const bool adv = issued < total;
+    const bool wrap = ls + 1 == Sp;
+    ls = adv ? (wrap ? 0 : ls + 1) : ls;
+    lchunk = (adv && wrap) ? lchunk + 4 : lchunk;
   };
   // Q14 limbs of the slab's [[R, I], [-I, R]] blocks (as the 16-beam kernel), under the voltage loads.  Pair e -> 4
   // consecutive slot antennas x beam row ml = (tid >> 2) % 32, slot antenna sa0 + 8 J.  The first batch's delay
@@ -492,7 +500,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
   if constexpr (!(Mode & 1)) batch_model(0, dv_first, gv_first);
   __builtin_amdgcn_sched_barrier(0);
 
-  uint32_t d0[8][2], d1[8][2], d2[8][2], d3[8][2];
+  u32x2_t d0[8], d1[8], d2[8], d3[8];
   issue(d0);
   issue(d1);
   issue(d2);
@@ -505,22 +513,22 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
     const int nj = 4 * Sp;  // 32 Sp slot antennas x 32 beams / 256 threads
     int cs0 = 0, cs1 = 0;
     const int off0 = coef8_byte(2 * sa0, 2 * ml, 4, 0);
+    // the model batches are software-pipelined: batch j0 + kBatch is requested before batch j0's phasors, so each
+    // batch's (L2) load latency hides under the previous batch's float64 work -- measured per wave (s_memtime,
+    // diagnostics Mode 128), four load-then-compute batches were 40 % of a wave's lifetime
+    float4 dv[kBatch];
+    float gv[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      dv[j] = dv_first[j];
+      gv[j] = gv_first[j];
+    }
     for (int j0 = 0; j0 < nj; j0 += kBatch) {
-      float4 dv[kBatch];
-      float gv[kBatch];
+      float4 dvn[kBatch];
+      float gvn[kBatch];
+      if constexpr (!(Mode & 1)) batch_model(j0 + kBatch, dvn, gvn);  // clamped: past the end it rereads the row
       bool valid[kBatch];
       int wc[kBatch], ws[kBatch];
-      if constexpr (!(Mode & 1)) {
-        if (j0 == 0) {
-#pragma unroll
-          for (int j = 0; j < kBatch; ++j) {
-            dv[j] = dv_first[j];
-            gv[j] = gv_first[j];
-          }
-        } else {
-          batch_model(j0, dv, gv);
-        }
-      }
 #pragma unroll
       for (int j = 0; j < kBatch; ++j) {
         const int sa = sa0 + 8 * (j0 + j), st = sa >> 5;
@@ -550,6 +558,13 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
         cs0 += Wc - Ws;
         cs1 += Ws + Wc;
       }
+      if constexpr (!(Mode & 1)) {
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+          dv[j] = dvn[j];
+          gv[j] = gvn[j];
+        }
+      }
     }
     if constexpr (!Signed) {
       cs0 += __shfl_xor(cs0, 1);
@@ -563,6 +578,10 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
     }
   }
   lds_barrier();  // the table is complete; the voltage prefetch stays in flight
+  if constexpr ((Mode & 128) != 0) {
+    st_m = __builtin_amdgcn_s_memtime();
+    st_c = st_m - st_t0;
+  }
 
   const float s32 = P.out_scale * 0x1p-14f;
   const int M2 = 2 * P.M;
@@ -578,6 +597,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
 #pragma unroll
         for (int t = 0; t < 4; ++t) hi[p][i][t] = lo[p][i][t] = i32x4_t{0, 0, 0, 0};
     // four steps in flight; a step's buffer is reloaded as soon as its fragments are built
+    if constexpr ((Mode & 128) != 0) st_m = __builtin_amdgcn_s_memtime();
     for (int s = 0; s < Sp; s += 4) {
       i32x4_t f[2][2];
       w32_frags<Signed>(d0, f);
@@ -592,6 +612,11 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
       w32_frags<Signed>(d3, f);
       issue(d3);
       w32_mfma<Mode>(lds4, s + 3, lane, f, hi, lo);
+    }
+    if constexpr ((Mode & 128) != 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      st_l += t - st_m;
+      st_m = t;
     }
     if constexpr (Mode & 4) {
       int sum = 0;
@@ -653,7 +678,21 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
         }
       }
     }
+    if constexpr ((Mode & 128) != 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      st_s += t - st_m;
+    }
     chunk += 4;
+  }
+  if constexpr ((Mode & 128) != 0) {
+    unsigned long long* o = reinterpret_cast<unsigned long long*>(const_cast<float*>(P.gain)) +
+                            (static_cast<size_t>(blockIdx.x) * 4 + wave) * 4;
+    if (lane == 0) {
+      o[0] = st_c;
+      o[1] = st_l;
+      o[2] = st_s;
+      o[3] = __builtin_amdgcn_s_memtime() - st_t0;
+    }
   }
 }
 
@@ -708,6 +747,30 @@ template int launch_i8_w32<true>(FusedArgs, hipStream_t);
 
 #ifdef BF_DIAG
 // Diagnostics: the integer wide kernel's ablations (tools/diag_fused.py, DIAG_KERNELS=w8).
+// Mode 128 of the 32-beam kernel writes per-wave phase cycles to `stamps` (uint64 [grid][4 waves][4]).
+extern "C" int bf_diag_w32_stamps(const uint8_t* raw, const float* dv, void* y, void* stamps, int B, int C, int T,
+                                  int A, int M, int Ctot, double ts, void* stream) {
+  bf::FusedArgs P{};
+  P.raw = raw;
+  P.dv = reinterpret_cast<const float4*>(dv);
+  P.y = y;
+  P.gain = reinterpret_cast<const float*>(stamps);  // Mode 128: not gains (the Gain instantiation is not used)
+  P.delay_channels = 1;
+  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
+  P.ctot = Ctot;
+  P.ts = ts;
+  P.k = -3.141592653589793 / (Ctot * ts);
+  P.batch_dt = 1e-3;
+  P.out_scale = 1.0f / 64;
+  P.nslabs = (M + 31) / 32;
+  P.xcd_order = P.nslabs > 1;
+  const long long items = static_cast<long long>(B) * C;
+  const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
+  hipLaunchKernelGGL((bf::beamform_fused_i8_w32_kernel<true, 128, false>), dim3(static_cast<unsigned>(grid)),
+                     dim3(bf::kW8Threads), bf::w32_lds_bytes(A), bf::as_stream(stream), P);
+  BF_LAUNCHED("beamform_fused_i8_w32_kernel");
+}
+
 extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y, int B, int C, int T, int A, int M,
                           int Ctot, double ts, void* stream) {
   bf::FusedArgs P{};

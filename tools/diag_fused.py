@@ -205,3 +205,18 @@ if "table" in _os.environ.get("DIAG_KERNELS", ""):  # the MatrixMultiply drop-in
         for mode, nm in tnames.items():
             t = timeit(lambda i: lib.bf_diag_table(mode, nts, xb.ptr, wt.ptr, yt.ptr, B, 2, C, T // 16, A, M, q.handle))
             print(f"  table nts={nts} mode {mode:2d} {nm:26s} {t*1e6:8.1f} us  alg {tb/t/1e9:7.1f} GB/s")
+if _os.environ.get("W32_STAMPS"):  # per-wave phase cycles of the 32-beam int8 kernel (s_memtime)
+    lib.bf_diag_w32_stamps.argtypes = [V, V, V, V, I, I, I, I, I, I, D, V]
+    Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
+    grid = (B * C + 7) // 8 * 8 * ((M + 31) // 32)
+    stamps = accel.DeviceArray(ctx, (grid * 4 * 4,), np.uint64)
+    for _ in range(3):  # clocks settle
+        assert lib.bf_diag_w32_stamps(bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, stamps.ptr, B, C, T, A, M, Ctot,
+                                      1 / 1712e6, q.handle) == 0
+    q.finish()
+    st = stamps.get(q).reshape(grid, 4, 4).astype(np.float64)
+    med = np.median(st.reshape(-1, 4), axis=0)
+    mean = st.reshape(-1, 4).mean(axis=0)
+    print(f"  w32 stamps (cycles per wave, median / mean over {grid * 4} waves): coefficient phase {med[0]:.0f} / "
+          f"{mean[0]:.0f}, contraction {med[1]:.0f} / {mean[1]:.0f}, requant+stores {med[2]:.0f} / {mean[2]:.0f}, "
+          f"total {med[3]:.0f} / {mean[3]:.0f}")
