@@ -74,6 +74,9 @@ def parse():
                    help="N > 1: how the full-band cube reaches the ranks (nccl = RCCL over xGMI, device to device; "
                         "gloo = host staging, for rehearsals with several ranks on one GPU; none = per-rank "
                         "synthetic input)")
+    p.add_argument("--scatter-at-one", action="store_true",
+                   help="run the scatter path at N = 1 as well (a one-rank RCCL communicator: exercises the device "
+                        "band, the collective call and the binding of the received tensor on a one-GPU box)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-secondary", action="store_true")
@@ -93,14 +96,17 @@ class Dist:
     channel scatter.  torch is imported before libbf, so one HIP runtime serves both (its libamdhip64 SONAME is
     the one libbf.so links)."""
 
-    def __init__(self, scatter_backend="none"):
+    def __init__(self, scatter_backend="none", force=False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.dist = None
-        self.scatter_backend = scatter_backend if self.world > 1 else "none"
+        self.scatter_backend = scatter_backend if (self.world > 1 or force) else "none"
         self.nccl = None
-        if self.world > 1:
+        if self.world > 1 or (force and scatter_backend != "none"):
+            os.environ.setdefault("MASTER_PORT", "29531")
+            os.environ.setdefault("WORLD_SIZE", str(self.world))
+            os.environ.setdefault("RANK", str(self.rank))
             import torch
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -474,7 +480,7 @@ def secondary(args, dist, workload, out_int8, int8_contract="q14"):
 def main():
     args = parse()
     wl = WORKLOADS[args.workload]
-    dist = Dist(args.scatter_backend)
+    dist = Dist(args.scatter_backend, force=args.scatter_at_one)
     from dpdk_dc_sand_amd import accel
 
     n_dev = accel.device_count()
@@ -488,7 +494,7 @@ def main():
     tmpl = template(args, dist, wl)
     scatter = None
     inputs = None
-    if dist.world > 1 and dist.scatter_backend != "none":
+    if dist.scatter_backend != "none":
         inputs, scatter = scatter_inputs(args, dist, tmpl.input_shape)
     r = run_gpu(args, dist, wl, tmpl=tmpl, inputs=inputs)
     total_samples = r["samples_per_step"] * args.steps * dist.world

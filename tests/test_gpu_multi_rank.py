@@ -118,3 +118,23 @@ def test_bench_multi_rank_rehearsal(tmp_path):
     assert line["scatter"]["backend"] == "gloo" and line["scatter"]["ranks"] == 2
     assert line["scatter"]["bytes_per_rank"] == 8 * 64 * 4096 * 256 * 4
     assert line["value"] > 0
+
+
+def test_bench_rccl_scatter_path_one_rank(tmp_path):
+    """The RCCL side of the channel scatter on a one-GPU box: a one-rank "nccl" communicator runs bench.py's device
+    path end to end -- band generated in HBM, packed slices, torch.distributed scatter over RCCL, the received
+    device tensor bound as the operator's input and timed.  (More ranks than GPUs is not an RCCL configuration; the
+    N-rank run is the driver's multi-GPU node.)"""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--settle-ms", "0",
+           "--scatter-backend", "nccl", "--scatter-at-one", "--workload", "cfg2", "--no-secondary", "--no-pmc",
+           "--no-cpu-baseline", "--no-ceiling"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    sc = line["scatter"]
+    assert sc["backend"] == "nccl" and sc["ranks"] == 1 and "RCCL" in sc["collective"], sc
+    assert sc["bytes_per_rank"] == 8 * 64 * 4096 * 256 * 4 and sc["seconds"] > 0
+    assert line["value"] > 0
