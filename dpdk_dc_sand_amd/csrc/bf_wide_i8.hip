@@ -1,4 +1,6 @@
 // Integer wide fused beamformer: many antennas x beams (config 4: 256 antennas, 64 beams), int8 beams, bit-exact.
+// Two kernels: the 32-beam slab kernel further down (the default, BF_FUSED_PATH_WIDE) and the 16-beam one here
+// (BF_FUSED_PATH_WIDE16, and shapes the 32-beam one does not fit).
 //
 // Same integer contract as beamform_fused_i8_item_kernel (oracle.fused_beamform_int8: Q14 coefficients of the
 // exact float32 phasors, exact int32 products, one float rounding to int8), organised like the float wide kernel

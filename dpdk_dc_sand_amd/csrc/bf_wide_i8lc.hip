@@ -1,6 +1,11 @@
 // Integer wide fused beamformer, loader/consumer form: many antennas x beams (config 4: 256 antennas, 64 beams),
 // int8 beams, bit-exact to the integer contract (oracle.fused_beamform_int8).
 //
+// STATUS: an explicit path only (BF_FUSED_PATH_STAGED, tested bit-exact); measured slower than the 32-beam slab
+// kernel of bf_wide_i8.hip, which is the default (827 vs ~520 us at config 4: one consumer wave per SIMD cannot
+// overlap its own VALU with its MFMAs, and one loader wave per SIMD could not build the tables fast enough --
+// per-phase s_memtime stamps in profiles/r2_lc_phase_stamps.txt).
+//
 // Why a second wide kernel.  The slab-per-workgroup kernel (bf_wide_i8.hip) reads each (batch, channel) item's
 // 256 KiB of voltages once per 16-beam slab (4x, the later reads from L2), keeps at most two k-steps of loads in
 // flight per wave and evaluates its phasors between its loads and its MFMAs; its load path alone (no coefficients, no
