@@ -424,7 +424,8 @@ __device__ __forceinline__ void w32_mfma(const int4* __restrict__ fr, int s, int
   }
 }
 
-// Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads.
+// Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads, 64 model loads
+// without the phasor math, 256 the phasor math on register-made delays (no model loads).
 template <bool Signed, int Mode = 0, bool Gain = false>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
@@ -490,6 +491,12 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
     for (int j = 0; j < kBatch; ++j) {
       const int sa = sa0 + 8 * (j0 + j), st = sa >> 5;
       const int a = min(w8_step_base(st, P.A) + (sa & 31), P.A - 1);
+      if constexpr ((Mode & 256) != 0) {  // diagnostics: no model loads, register-made delays (same math after)
+        const float u = static_cast<float>(a * 37 + ml * 11 + j0);
+        dv[j] = float4{u * 1e-10f, 0.0f, u * 1e-3f - 3.0f, 0.0f};
+        gv[j] = 1.0f;
+        continue;
+      }
       dv[j] = dv_row[a];
       if constexpr (Gain)
         gv[j] = g_row[a];
@@ -542,6 +549,12 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
         for (int j = 0; j < kBatch; ++j) {
           wc[j] = valid[j] ? 8192 + 16 * j + tid : 0;
           ws[j] = valid[j] ? 4096 - 16 * j : 0;
+        }
+      } else if constexpr ((Mode & 64) != 0) {  // diagnostics: model loads kept, a few VALU instead of the phasors
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+          wc[j] = valid[j] ? (static_cast<int>(dv[j].x * 1e12f + dv[j].y) & 8191) : 0;
+          ws[j] = valid[j] ? (static_cast<int>(dv[j].z * 1e3f + dv[j].w) & 8191) : 0;
         }
       } else {
         q14_coeffs<kBatch, true, false, true>(dv, gv, valid, ch, P.ctot, P.ts, P.k, dt, P.gain, wc, ws);
@@ -820,6 +833,8 @@ extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y
     case 1013: return bf::launch_w32<true, 13>(P, st);
     case 1016: return bf::launch_w32<true, 16>(P, st);
     case 1017: return bf::launch_w32<true, 17>(P, st);
+    case 1064: return bf::launch_w32<true, 64>(P, st);    // model loads, no phasor math
+    case 1256: return bf::launch_w32<true, 256>(P, st);   // phasor math, no model loads
     default: return BF_ERR_ARG;
   }
 }

@@ -19,5 +19,5 @@ for line in out.splitlines():
         cur[k.strip()] = v.strip()
 for r in rows:
     n = subprocess.run(["c++filt"], input=r["name"], capture_output=True, text=True).stdout.strip()
-    n = re.sub(r"\(.*", "", n).replace("bf::(anonymous namespace)::", "")
-    print(f"{n[:70]:70s} V={r.get('VGPRs')} A={r.get('AGPRs')} S={r.get('SGPRs')} scr={r.get('ScratchSize [bytes/lane]')} occ={r.get('Occupancy [waves/SIMD]')}")
+    n = re.sub(r"\(.*", "", n.replace("bf::(anonymous namespace)::", "").replace("void ", ""))
+    print(f"{n[:90]:90s} V={r.get('VGPRs')} A={r.get('AGPRs')} S={r.get('SGPRs')} scr={r.get('ScratchSize [bytes/lane]')} occ={r.get('Occupancy [waves/SIMD]')}")
