@@ -167,7 +167,14 @@ __global__ __launch_bounds__(kThreads) void beamform_table_kernel(const uint8_t*
 // (address clamped inside the table; steps past S meet zero coefficients).  The loop body is identical every
 // iteration, so the compiler's vmcnt waits stay exact and R G loads stay in flight -- the per-step load-then-use of
 // the basic kernel paid one memory latency per k-step (32 per row at 256 antennas).
-template <bool Signed, int NTS, int R, int Mode = 0>
+//
+// W16 (A % 8 == 0, x 16-byte aligned): one 16-byte load per lane covers two k-steps -- lane group h reads bytes
+// [64 s2 + 16 h, + 16) of its row, i.e. halves (A_h, B_h) -- and two permlane swaps per dword rebuild both steps'
+// fragments exactly:  permlane16_swap(A, B) -> ([A0 B0 A2 B2], [A1 B1 A3 B3]) over lane groups 0..3, then
+// permlane32_swap -> step 2 s2 = [A0 B0 A1 B1] (k = 8 h + j) and step 2 s2 + 1 = [A2 B2 A3 B3].  Half the load
+// instructions (each still touches 16 row segments), the same per-step fragments and MFMA order (bitwise the same
+// sums as the 8-byte form, and as the fused kernels).
+template <bool Signed, int NTS, int R, int Mode = 0, bool W16 = false>
 __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uint8_t* __restrict__ x,
                                                                        const float* __restrict__ w,
                                                                        float* __restrict__ y, int NB, int A, int M,
@@ -202,6 +209,11 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
     if constexpr (Mode & 8) return uint2{static_cast<uint32_t>(s + tl), static_cast<uint32_t>(s)};
     return *reinterpret_cast<const uint2*>(row + min(32 * s + kh, K2 - 8));
   };
+  auto ld16 = [&](const uint8_t* row, int s2) -> uint4 {  // W16: steps 2 s2, 2 s2 + 1
+    if constexpr (Mode & 8)
+      return uint4{static_cast<uint32_t>(s2 + tl), static_cast<uint32_t>(s2), static_cast<uint32_t>(s2 - tl), 7u};
+    return *reinterpret_cast<const uint4*>(row + min(64 * s2 + 2 * kh, K2 - 16));
+  };
   const uint8_t* cur_rows[G];
   const uint8_t* next_rows[G];
 #pragma unroll
@@ -211,11 +223,20 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
   }
   // the ring's first R steps are requested BEFORE the coefficient table: vmcnt counts in order, so the table
   // conversion's wait then covers both, and the voltage latency overlaps the table's
-  uint2 ring[R][G];
+  constexpr int R8 = W16 ? 1 : R, R16 = W16 ? R / 2 : 1;
+  uint2 ring[R8][G];
+  uint4 ring16[R16][G];
+  if constexpr (W16) {
 #pragma unroll
-  for (int r = 0; r < R; ++r)
+    for (int r = 0; r < R16; ++r)
 #pragma unroll
-    for (int g = 0; g < G; ++g) ring[r][g] = ld(cur_rows[g], r);
+      for (int g = 0; g < G; ++g) ring16[r][g] = ld16(cur_rows[g], r);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int g = 0; g < G; ++g) ring[r][g] = ld(cur_rows[g], r);
+  }
   __builtin_amdgcn_sched_barrier(0);
   // Mode (diagnostics only): 1 no table staging, 2 no MFMA, 4 no stores, 8 no voltage loads
   if constexpr (!(Mode & 1))
@@ -234,16 +255,7 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
     for (int s0 = 0; s0 < Sp; s0 += R) {  // R divides Sp
       const bool nx = s0 + R >= Sp;      // this ring turn prefetches the next row groups' first steps
       const int sb = nx ? 0 : s0 + R;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        half8 v[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const uint2 cur = ring[r][g];
-          ring[r][g] = ld(nx ? next_rows[g] : cur_rows[g], sb + r);
-          v[g] = bytes8_to_frag<Signed>(cur.x, cur.y);
-        }
-        const int s = s0 + r;
+      auto contract = [&](int s, const half8 (&v)[G]) {
 #pragma unroll
         for (int tau = 0; tau < NTS; ++tau) {
           if (tau < nts) {
@@ -259,6 +271,37 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
               }
             }
           }
+        }
+      };
+      if constexpr (W16) {
+#pragma unroll
+        for (int r = 0; r < R16; ++r) {
+          half8 v0[G], v1[G];
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const uint4 cur = ring16[r][g];
+            ring16[r][g] = ld16(nx ? next_rows[g] : cur_rows[g], sb / 2 + r);
+            auto x0 = __builtin_amdgcn_permlane16_swap(cur.x, cur.z, false, false);
+            auto x1 = __builtin_amdgcn_permlane16_swap(cur.y, cur.w, false, false);
+            auto y0 = __builtin_amdgcn_permlane32_swap(x0[0], x0[1], false, false);
+            auto y1 = __builtin_amdgcn_permlane32_swap(x1[0], x1[1], false, false);
+            v0[g] = bytes8_to_frag<Signed>(y0[0], y1[0]);
+            v1[g] = bytes8_to_frag<Signed>(y0[1], y1[1]);
+          }
+          contract(s0 + 2 * r, v0);
+          contract(s0 + 2 * r + 1, v1);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          half8 v[G];
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const uint2 cur = ring[r][g];
+            ring[r][g] = ld(nx ? next_rows[g] : cur_rows[g], sb + r);
+            v[g] = bytes8_to_frag<Signed>(cur.x, cur.y);
+          }
+          contract(s0 + r, v);
         }
       }
     }
@@ -298,7 +341,7 @@ int launch_table(const uint8_t* x, const float* w, float* y, long long bpc, int 
   BF_LAUNCHED("beamform_table_kernel");
 }
 
-template <bool Signed, int NTS, int R, int Mode = 0>
+template <bool Signed, int NTS, int R, int Mode = 0, int Form = 0>
 int launch_ring(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                 hipStream_t st) {
   const int nslabs = (NT + NTS - 1) / NTS;
@@ -308,9 +351,14 @@ int launch_ring(const uint8_t* x, const float* w, float* y, long long bpc, int N
   const int xcd = nslabs > 1;
   const long long grid = xcd ? (bpc + 7) / 8 * 8 * nslabs : bpc * nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform: grid too large");
-  hipLaunchKernelGGL((beamform_table_ring_kernel<Signed, NTS, R, Mode>), dim3(static_cast<unsigned>(grid)),
-                     dim3(kThreads),
-                     lds, st, x, w, y, NB, A, M, S, NT, nslabs, bpc, xcd);
+  // Form 0: 16-byte loads when the rows allow them (A % 8 == 0, x 16-byte aligned); 1 (diagnostics): 8-byte loads
+  const bool w16 = Form == 0 && A % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  if (w16)
+    hipLaunchKernelGGL((beamform_table_ring_kernel<Signed, NTS, R, Mode, true>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kThreads), lds, st, x, w, y, NB, A, M, S, NT, nslabs, bpc, xcd);
+  else
+    hipLaunchKernelGGL((beamform_table_ring_kernel<Signed, NTS, R, Mode>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kThreads), lds, st, x, w, y, NB, A, M, S, NT, nslabs, bpc, xcd);
   BF_LAUNCHED("beamform_table_ring_kernel");
 }
 
@@ -392,6 +440,12 @@ extern "C" int bf_diag_table(int mode, int nts, const uint8_t* x, const float* w
     BF_TABLE_MODE(9);
     BF_TABLE_MODE(6);
     BF_TABLE_MODE(7);
+    case 100:  // the 8-byte-load form (A/B against mode 0)
+      return nts == 4 ? bf::launch_ring<true, 4, 16, 0, 1>(x, w, y, bpc, NB, A, M, S, NT, st)
+                      : bf::launch_ring<true, 2, 16, 0, 1>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 108:
+      return nts == 4 ? bf::launch_ring<true, 4, 16, 8, 1>(x, w, y, bpc, NB, A, M, S, NT, st)
+                      : bf::launch_ring<true, 2, 16, 8, 1>(x, w, y, bpc, NB, A, M, S, NT, st);
     default: return BF_ERR_ARG;
   }
 #undef BF_TABLE_MODE

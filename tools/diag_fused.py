@@ -201,10 +201,18 @@ if "table" in _os.environ.get("DIAG_KERNELS", ""):  # the MatrixMultiply drop-in
     yt = accel.DeviceArray(ctx, (B * 2 * C * T * 2 * M,), np.float32)
     _lib.call("bf_memset", wt.ptr, 0, wt.nbytes if hasattr(wt, "nbytes") else B * 2 * C * 2 * A * 2 * M * 4, q.handle)
     tb = 2 * B * 2 * C * T * A + B * 2 * C * 2 * A * 2 * M * 4 + B * 2 * C * T * 2 * M * 4
-    for nts in (2, 4):
+    tnames.update({100: "8-byte loads (full)", 108: "8-byte loads, no x loads"})
+    if _os.environ.get("TABLE_MODES"):  # e.g. 0,100: interleaved A/B over DIAG_ROUNDS, medians
+        tnames = {int(m): tnames.get(int(m), str(m)) for m in _os.environ["TABLE_MODES"].split(",")}
+    for nts in [int(v) for v in _os.environ.get("TABLE_NTS", "2,4").split(",")]:
+        res = {m: [] for m in tnames}
+        for r in range(ROUNDS):
+            for mode in tnames:
+                res[mode].append(timeit(lambda i: lib.bf_diag_table(mode, nts, xb.ptr, wt.ptr, yt.ptr, B, 2, C, T // 16,
+                                                                    A, M, q.handle)))
         for mode, nm in tnames.items():
-            t = timeit(lambda i: lib.bf_diag_table(mode, nts, xb.ptr, wt.ptr, yt.ptr, B, 2, C, T // 16, A, M, q.handle))
-            print(f"  table nts={nts} mode {mode:2d} {nm:26s} {t*1e6:8.1f} us  alg {tb/t/1e9:7.1f} GB/s")
+            t = sorted(res[mode])[len(res[mode]) // 2]
+            print(f"  table nts={nts} mode {mode:3d} {nm:26s} {t*1e6:8.1f} us  alg {tb/t/1e9:7.1f} GB/s")
 if _os.environ.get("W32_STAMPS"):  # per-wave phase cycles of the 32-beam int8 kernel (s_memtime)
     lib.bf_diag_w32_stamps.argtypes = [V, V, V, V, I, I, I, I, I, I, D, V]
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
