@@ -26,6 +26,7 @@
 //                             contiguous, so a 16-byte load = 4 samples x 2 pols of one antenna and the
 //                             reorder costs no HBM traffic), W generated in float64 in-kernel per (b, c) from
 //                             the delay model.  One workgroup per (b, c[, slab]), both pols.
+#include <algorithm>
 #include <cstdlib>
 
 #include "bf_mfma.hpp"
@@ -202,8 +203,8 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
   auto rowp = [&](int j) -> const uint8_t* {  // clamped inside the item even for row-less waves
     return xp + static_cast<size_t>(min((wave + kWaves * j) * kSamplesPerBlock + tl, T - 1)) * K2;
   };
-  // (a 16-byte, two-step load per lane would permute the k summation order, and the fused kernels' bitwise
-  // equality with this chain rests on the same order: 8-byte, one-step loads)
+  // (the fused kernels' bitwise equality with this chain rests on the per-step fragments: the 16-byte form below
+  // re-deals its loads into exactly the one-step fragments)
   const int kh = 8 * h;
   auto ld = [&](const uint8_t* row, int s) -> uint2 {
     if constexpr (Mode & 8) return uint2{static_cast<uint32_t>(s + tl), static_cast<uint32_t>(s)};
@@ -327,6 +328,192 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
   }
 }
 
+// Persistent form of the 16-byte ring kernel (256-antenna rows: UPT = 8 table units per thread): a workgroup walks
+// its (item, slab) list, and the next item's coefficient slab is loaded into registers (64 floats per thread) while
+// the current item is contracted, so the table read -- half the algorithmic bytes at config 4 -- no longer sits
+// between the workgroup's start and its first MFMA.  The ring's last turn of an item prefetches the next item's
+// first steps.  Per item: convert the registers into the LDS slab, barrier, request the next slab, contract, barrier.
+// The MFMA sequence per output is the ring kernel's (bitwise the same results).
+template <bool Signed, int NTS, int R, int UPT, int Mode = 0>
+__global__ __launch_bounds__(kThreads, 2) void beamform_table_persist_kernel(
+    const uint8_t* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int NB, int A, int M, int S,
+    int NT, int nslabs, long long nbpc, int xcd, long long nitems) {
+  extern __shared__ __attribute__((aligned(16))) half8 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const int K2 = 2 * A, M2 = 2 * M;
+  const int Sp = (S + R - 1) / R * R;
+  const int T = NB * kSamplesPerBlock;
+  constexpr int G = 2, R16 = R / 2, cols = NTS * 16;
+  const long long stride = gridDim.x;  // a multiple of 8: an item's XCD is its workgroup's
+  // item -> (slab, bpc), the table_coords mapping; padding items (xcd groups past nbpc) are skipped
+  auto coords = [&](long long it, int& slab, size_t& bpc) -> bool {
+    if (xcd) {
+      const long long local = it >> 3;
+      slab = static_cast<int>(local % nslabs);
+      bpc = static_cast<size_t>(local / nslabs) * 8 + static_cast<size_t>(it & 7);
+    } else {
+      slab = static_cast<int>(it % nslabs);
+      bpc = static_cast<size_t>(it / nslabs);
+    }
+    return static_cast<long long>(bpc) < nbpc;
+  };
+  auto next_valid = [&](long long it) -> long long {  // the first valid item >= it on this workgroup's list, or -1
+    int sl;
+    size_t bp;
+    for (; it < nitems; it += stride)
+      if (coords(it, sl, bp)) return it;
+    return -1;
+  };
+  float tv[UPT][8];
+  auto table_load = [&](int slab, size_t bpc) {
+    const float* wp = w + bpc * static_cast<size_t>(K2) * M2;
+    const int tau0 = slab * NTS;
+    // rows past 2A only occur as whole 8-row units (A % 8 == 0): clamp the unit's first row, zeroed at the store
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      const int e = u * kThreads + tid, kb = e / cols, cl = e % cols;
+      const float* pu = wp + static_cast<size_t>(min(8 * kb, K2 - 8)) * M2 + min(tau0 * 16 + cl, M2 - 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tv[u][j] = pu[static_cast<size_t>(j) * M2];
+    }
+  };
+  auto table_store = [&](int slab) {
+    const int tau0 = slab * NTS, nts = min(NTS, NT - tau0);
+    _Float16* lh = reinterpret_cast<_Float16*>(lds);
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      const int e = u * kThreads + tid, kb = e / cols, cl = e % cols;
+      if (cl >= 16 * nts) continue;
+      const bool colok = tau0 * 16 + cl < M2;
+      half8 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float wv = (colok && 8 * kb + j < K2) ? tv[u][j] : 0.0f;
+        hi[j] = static_cast<_Float16>(wv);
+        lo[j] = static_cast<_Float16>(wv - static_cast<float>(hi[j]));
+      }
+      const int e8 = coef_elem(8 * kb, cl, nts);
+      *reinterpret_cast<half8*>(lh + e8) = hi;
+      *reinterpret_cast<half8*>(lh + e8 + 64 * 8) = lo;
+    }
+  };
+  const int nrg = (NB - wave + kWaves - 1) / kWaves;
+  const int npair = (nrg + G - 1) / G;
+  // row pointer of the wave's row group j of item bpc (clamped inside the item)
+  auto rowp = [&](size_t bpc, int j) -> const uint8_t* {
+    return x + bpc * static_cast<size_t>(T) * K2 +
+           static_cast<size_t>(min((wave + kWaves * j) * kSamplesPerBlock + tl, T - 1)) * K2;
+  };
+  const int kh2 = 16 * h;
+  auto ld16 = [&](const uint8_t* row, int s2) -> uint4 {
+    if constexpr (Mode & 8)
+      return uint4{static_cast<uint32_t>(s2 + tl), static_cast<uint32_t>(s2), static_cast<uint32_t>(s2 - tl), 7u};
+    return *reinterpret_cast<const uint4*>(row + min(64 * s2 + kh2, K2 - 16));
+  };
+
+  long long it = next_valid(blockIdx.x);
+  if (it < 0) return;  // workgroup-uniform
+  int slab;
+  size_t bpc;
+  coords(it, slab, bpc);
+  long long itn = next_valid(it + stride);
+  int slab_n = slab;
+  size_t bpc_n = bpc;
+  if (itn >= 0) coords(itn, slab_n, bpc_n);
+  table_load(slab, bpc);
+  const uint8_t* cur_rows[G];
+  const uint8_t* next_rows[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    cur_rows[g] = rowp(bpc, g);
+    next_rows[g] = npair > 1 ? rowp(bpc, G + g) : rowp(bpc_n, g);
+  }
+  uint4 ring16[R16][G];
+#pragma unroll
+  for (int r = 0; r < R16; ++r)
+#pragma unroll
+    for (int g = 0; g < G; ++g) ring16[r][g] = ld16(cur_rows[g], r);
+
+  while (true) {
+    __syncthreads();  // every wave is done reading the previous slab
+    if constexpr (!(Mode & 1)) table_store(slab);
+    __syncthreads();
+    if (itn >= 0) table_load(slab_n, bpc_n);  // in flight during this item's contraction
+    const int tau0 = slab * NTS, nts = min(NTS, NT - tau0);
+    float* yp = y + bpc * static_cast<size_t>(T) * M2;
+    for (int pi = 0; pi < npair; ++pi) {
+      f32x4 acc[G][NTS];
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau) acc[g][tau] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s0 = 0; s0 < Sp; s0 += R) {
+        const bool nx = s0 + R >= Sp;
+        const int sb = nx ? 0 : s0 + R;
+#pragma unroll
+        for (int r = 0; r < R16; ++r) {
+          half8 v0[G], v1[G];
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const uint4 cur = ring16[r][g];
+            ring16[r][g] = ld16(nx ? next_rows[g] : cur_rows[g], sb / 2 + r);
+            auto x0 = __builtin_amdgcn_permlane16_swap(cur.x, cur.z, false, false);
+            auto x1 = __builtin_amdgcn_permlane16_swap(cur.y, cur.w, false, false);
+            auto y0 = __builtin_amdgcn_permlane32_swap(x0[0], x0[1], false, false);
+            auto y1 = __builtin_amdgcn_permlane32_swap(x1[0], x1[1], false, false);
+            v0[g] = bytes8_to_frag<Signed>(y0[0], y1[0]);
+            v1[g] = bytes8_to_frag<Signed>(y0[1], y1[1]);
+          }
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int s = s0 + 2 * r + half;
+#pragma unroll
+            for (int tau = 0; tau < NTS; ++tau) {
+              if (tau < nts) {
+                const int slot = ((s * nts + tau) * 2) * 64;
+                const half8 chi = lds[slot + lane], clo = lds[slot + 64 + lane];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                  const half8 vv = half ? v1[g] : v0[g];
+                  acc[g][tau] = mfma(chi, vv, acc[g][tau]);
+                  acc[g][tau] = mfma(clo, vv, acc[g][tau]);
+                }
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int j = pi * G + g;
+        if (j >= nrg) break;
+        float* orow = yp + static_cast<size_t>((wave + kWaves * j) * kSamplesPerBlock + tl) * M2;
+#pragma unroll
+        for (int tau = 0; tau < NTS; ++tau)
+          if (tau < nts) store_f32<NTS>(orow, 16 * (tau0 + tau) + 4 * h, M2, acc[g][tau]);
+      }
+      // rows of pair pi + 2: this item's, or (past its last pair) the next item's first pairs
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        cur_rows[g] = next_rows[g];
+        const int q = pi + 2;
+        next_rows[g] = q < npair ? rowp(bpc, q * G + g) : rowp(bpc_n, (q - npair) * G + g);
+      }
+    }
+    if (itn < 0) break;  // workgroup-uniform
+    it = itn;
+    slab = slab_n;
+    bpc = bpc_n;
+    itn = next_valid(it + stride);
+    if (itn >= 0) coords(itn, slab_n, bpc_n);
+    if (npair == 1) {  // the pair-end update above already moved to this item; its next pair is the following item's
+#pragma unroll
+      for (int g = 0; g < G; ++g) next_rows[g] = rowp(bpc_n, g);
+    }
+  }
+}
+
 template <bool Signed, int NTS, bool Vec8>
 int launch_table(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                  hipStream_t st) {
@@ -362,14 +549,46 @@ int launch_ring(const uint8_t* x, const float* w, float* y, long long bpc, int N
   BF_LAUNCHED("beamform_table_ring_kernel");
 }
 
+// The persistent ring kernel: UPT table units per thread (Sp * NTS / 4 == UPT), two workgroups per CU.
+template <bool Signed, int NTS, int R, int UPT, int Mode = 0>
+int launch_persist(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
+                   hipStream_t st) {
+  const int nslabs = (NT + NTS - 1) / NTS;
+  const int Sp = (S + R - 1) / R * R;
+  const size_t lds = coef_lds_bytes(Sp, NTS);
+  BF_REQUIRE(lds <= kMaxLds / 2 && Sp * NTS == 4 * UPT && A % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+             "bf_beamform: shape does not fit the persistent table kernel");
+  const int xcd = nslabs > 1;
+  const long long nitems = xcd ? (bpc + 7) / 8 * 8 * nslabs : bpc * nslabs;
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0, n = 0;
+    BF_HIP(hipGetDevice(&dev));
+    BF_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    n_cu = n > 0 ? n : 256;
+  }
+  const long long grid = std::min<long long>(nitems, 2LL * n_cu / 8 * 8);  // a multiple of 8 (item XCD = workgroup's)
+  BF_REQUIRE(grid > 0 && grid % 8 == 0, "bf_beamform: persistent grid");
+  hipLaunchKernelGGL((beamform_table_persist_kernel<Signed, NTS, R, UPT, Mode>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kThreads), lds, st, x, w, y, NB, A, M, S, NT, nslabs, bpc, xcd, nitems);
+  BF_LAUNCHED("beamform_table_persist_kernel");
+}
+
 template <bool Signed, int NTS>
 int dispatch_vec(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                  hipStream_t st) {
   const char* e = diag_env("BF_TABLE_BASIC");  // tests: force the basic kernel
   if (A % 4 == 0 && !(e && e[0] == '1')) {
     // ring depth: the k-steps of a row, up to 16 (the steps are padded to a multiple of R); long rows only
-    if (S >= 16 && coef_lds_bytes((S + 15) / 16 * 16, NTS) <= kMaxLds)
+    if (S >= 16 && coef_lds_bytes((S + 15) / 16 * 16, NTS) <= kMaxLds) {
+      // 256-antenna rows in two-workgroup slabs (config 4): the persistent form, the next slab loaded under the
+      // current item's contraction
+      if constexpr (NTS == 2)
+        if ((S + 15) / 16 == 1 && A % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+            (bpc >= 8))
+          return launch_persist<Signed, 2, 16, 8>(x, w, y, bpc, NB, A, M, S, NT, st);
       return launch_ring<Signed, NTS, 16>(x, w, y, bpc, NB, A, M, S, NT, st);
+    }
     if (S >= 8 && coef_lds_bytes((S + 7) / 8 * 8, NTS) <= kMaxLds)
       return launch_ring<Signed, NTS, 8>(x, w, y, bpc, NB, A, M, S, NT, st);
     // 4..7 k-steps (64 antennas: config 3): a 4-deep ring
@@ -440,6 +659,11 @@ extern "C" int bf_diag_table(int mode, int nts, const uint8_t* x, const float* w
     BF_TABLE_MODE(9);
     BF_TABLE_MODE(6);
     BF_TABLE_MODE(7);
+    case 200:  // the persistent form (A/B against mode 0)
+      return nts == 2 ? bf::launch_persist<true, 2, 16, 8>(x, w, y, bpc, NB, A, M, S, NT, st) : BF_ERR_ARG;
+    case 300:  // the non-persistent 16-byte ring
+      return nts == 4 ? bf::launch_ring<true, 4, 16>(x, w, y, bpc, NB, A, M, S, NT, st)
+                      : bf::launch_ring<true, 2, 16>(x, w, y, bpc, NB, A, M, S, NT, st);
     case 100:  // the 8-byte-load form (A/B against mode 0)
       return nts == 4 ? bf::launch_ring<true, 4, 16, 0, 1>(x, w, y, bpc, NB, A, M, S, NT, st)
                       : bf::launch_ring<true, 2, 16, 0, 1>(x, w, y, bpc, NB, A, M, S, NT, st);

@@ -216,6 +216,31 @@ def test_matrix_multiply_random_tables(context, command_queue, A, M, C, T, signe
     assert_beams_allclose(y, O.complex_mult(x, w, signed=signed), x, w, signed=signed)
 
 
+@pytest.mark.parametrize("T,signed", [(32, True), (256, False)])
+def test_matrix_multiply_persistent_equals_ring(context, command_queue, T, signed):
+    """256 antennas in two-workgroup slabs with >= 8 (b, p, c) items take the persistent table kernel (the next
+    slab loaded under the current item, the ring's last turn prefetching the next item's rows; 640 slab items here,
+    more than one per workgroup, xcd padding items skipped).  Its per-item MFMA sequence is the ring kernel's, which
+    one-channel calls (4 items) still take: the results must be identical bits, and within tolerance of the oracle.
+    T = 32 leaves two of the four waves without row groups; T = 256 gives each wave two row-group pairs."""
+    B, A, M, C = 2, 256, 64, 40
+    rng = np.random.default_rng(T + 5)
+    x = rng.integers(0, 256, (B, 2, C, T // 16, 16, A, 2), dtype=np.uint8)
+    if signed:
+        x = x.view(np.int8)
+    w = rng.uniform(-1.0, 1.0, (B, 2, C, 2 * A, 2 * M)).astype(np.float32)
+    op = MatrixMultiplyTemplate(context, A, C, T, M, B, sample_signed=signed).instantiate(command_queue)
+    (y,) = run(op, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
+    one = MatrixMultiplyTemplate(context, A, 1, T, M, B, sample_signed=signed).instantiate(command_queue)
+    for c in (0, 1, 17, C - 1):
+        (yc,) = run(one, command_queue, {"inData": np.ascontiguousarray(x[:, :, c:c + 1]),
+                                          "inCoeffs": np.ascontiguousarray(w[:, :, c:c + 1])}, ["outData"])
+        np.testing.assert_array_equal(y[:, :, c:c + 1], yc)
+    sel = [0, 9, 23, C - 1]
+    xs, ws = np.ascontiguousarray(x[:, :, sel]), np.ascontiguousarray(w[:, :, sel])
+    assert_beams_allclose(y[:, :, sel], O.complex_mult(xs, ws, signed=signed), xs, ws, signed=signed)
+
+
 # ---- full sequence (beamform_op_sequence_test.py:37-200) ---------------------------------------------------
 def test_op_sequence_golden(context, command_queue):
     B, A, M, Ctot, T, C = (int(v) for v in get("opseq_cfg1", "dims"))
