@@ -6,8 +6,8 @@ CSRC     := dpdk_dc_sand_amd/csrc
 LIB      := dpdk_dc_sand_amd/libbf.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -munsafe-fp-atomics
 SRCS     := $(CSRC)/bf_runtime.cpp $(CSRC)/bf_coeff.hip $(CSRC)/bf_reorder.hip $(CSRC)/bf_beamform.hip \
-            $(CSRC)/bf_fused.hip $(CSRC)/bf_wide.hip $(CSRC)/bf_wide_i8.hip $(CSRC)/bf_wide_i8lc.hip $(CSRC)/bf_requant.hip \
-            $(CSRC)/bf_pipeline.cpp
+            $(CSRC)/bf_fused.hip $(CSRC)/bf_wide.hip $(CSRC)/bf_wide_i8.hip $(CSRC)/bf_requant.hip \
+            $(CSRC)/bf_pipeline.cpp $(CSRC)/bf_comm.cpp
 OBJS     := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 HDRS     := $(wildcard $(CSRC)/*.hpp) include/bf.h
 
@@ -35,7 +35,7 @@ build/%.o: $(CSRC)/% $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -ldl
 
 clean:
 	rm -rf build $(LIB)
@@ -45,4 +45,4 @@ DIAG_LIB := build/libbf_diag.so
 diag: $(DIAG_LIB)
 $(DIAG_LIB): $(SRCS) $(HDRS)
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -DBF_DIAG -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -DBF_DIAG -shared -o $@ $(SRCS) -ldl

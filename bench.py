@@ -13,10 +13,13 @@ requantised from the float32 path).  cfg2 (configs[1]): 1 beam.  cfg4 (configs[3
 
 Multi-GPU: frequency channels shard across ranks with no data-path collective (rank r = X-engine r,
 channels [C r, C (r+1)) of a C*N-channel band): scaling is weak.  The only collective is the root -> ranks channel
-scatter of the full-band voltage cube, over RCCL (`torch.distributed` backend "nccl") on the GPUs: rank 0 builds
-the band in its HBM, packs each rank's channel slice contiguously and scatters it; each rank's timed hot path then
-runs on the slice it received.  The scatter is timed on its own (outside the hot-path timing) and reported in the
-line's `scatter` block.  The timing bracket (barrier + max over ranks) runs over gloo.
+scatter of the full-band voltage cube, device to device over RCCL/xGMI through libbf (bf_channel_scatter): rank 0
+fills the band in its HBM, packs each rank's channel slice and sends it; each rank receives its slice straight into
+the fused operator's input buffer and its timed hot path runs on it.  The scatter is timed on its own (outside the
+hot-path timing) and reported in the line's `scatter` block.  The timing bracket (barrier + max over ranks) and the
+RCCL id hand-out run over a plain TCP group (dpdk_dc_sand_amd.rendezvous): no torch in the ranks, so every rank
+runs libbf on one HIP runtime.  At N > 1 the line's `secondary` also times config 4 channel-sharded (256 ants,
+64 beams, 4096 channels per rank of the 32768-channel band, xeng_id = rank: BASELINE configs[3] at N = 8).
 
 Rank 0 prints ONE JSON line.  `value` = samples all ranks processed / max-over-ranks wall time of the K timed
 steps (barrier + device sync on both sides).  `roofline.achieved` = algorithmic bytes per launch / average
@@ -70,18 +73,23 @@ def parse():
                    help="untimed clock-settle launches after the warmup steps (milliseconds of wall time)")
     p.add_argument("--unsigned", action="store_true", help="uint8 voltages (the reference slots' dtype) instead of int8")
     p.add_argument("--nbuf", type=int, default=2, help="rotating input/output buffer sets (defeat the 256 MB MALL)")
-    p.add_argument("--scatter-backend", choices=("nccl", "gloo", "none"), default="nccl",
-                   help="N > 1: how the full-band cube reaches the ranks (nccl = RCCL over xGMI, device to device; "
-                        "gloo = host staging, for rehearsals with several ranks on one GPU; none = per-rank "
-                        "synthetic input)")
+    p.add_argument("--scatter-backend", choices=("rccl", "host", "none", "nccl", "gloo"), default="rccl",
+                   help="N > 1: how the full-band cube reaches the ranks (rccl = libbf bf_channel_scatter over "
+                        "RCCL/xGMI, device to device; host = TCP through host memory, for rehearsals with several "
+                        "ranks on one GPU; none = per-rank synthetic input; nccl / gloo: aliases of rccl / host)")
     p.add_argument("--scatter-at-one", action="store_true",
                    help="run the scatter path at N = 1 as well (a one-rank RCCL communicator: exercises the device "
-                        "band, the collective call and the binding of the received tensor on a one-GPU box)")
+                        "band, the libbf scatter and the binding of the received slice on a one-GPU box)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-secondary", action="store_true")
     p.add_argument("--no-ceiling", action="store_true")
+    p.add_argument("--no-rocprof", action="store_true",
+                   help="skip the rocprofv3 --kernel-trace re-run that checks the event timings (rank 0, N = 1)")
+    p.add_argument("--prof-out", default=None,
+                   help="directory for that re-run's trace, timed_kernel_stats.csv and prof_bench.json")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--prof-child", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args()
     if a.out_f32:
         a.output = "f32"
@@ -92,53 +100,37 @@ def parse():
 
 
 class Dist:
-    """Barrier + max-reduction across ranks (gloo, CPU) for the timing bracket, plus an RCCL group for the
-    channel scatter.  torch is imported before libbf, so one HIP runtime serves both (its libamdhip64 SONAME is
-    the one libbf.so links)."""
+    """The ranks' host-side group (rendezvous.HostGroup over TCP: barrier + max for the timing bracket, the RCCL id
+    hand-out, the host scatter) and, for the RCCL channel scatter, libbf's communicator (shard.ChannelScatter,
+    opened once the rank's device is current).  No torch."""
 
-    def __init__(self, scatter_backend="none", force=False):
+    def __init__(self, scatter_backend="rccl", force=False):
+        from dpdk_dc_sand_amd.rendezvous import HostGroup
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.dist = None
-        self.scatter_backend = scatter_backend if (self.world > 1 or force) else "none"
-        self.nccl = None
-        if self.world > 1 or (force and scatter_backend != "none"):
-            os.environ.setdefault("MASTER_PORT", "29531")
-            os.environ.setdefault("WORLD_SIZE", str(self.world))
-            os.environ.setdefault("RANK", str(self.rank))
-            import torch
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            saved = os.dup(1)  # gloo prints its connection banner on stdout: keep stdout for the JSON line
-            os.dup2(2, 1)
-            try:
-                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
-                if self.scatter_backend == "nccl":
-                    torch.cuda.set_device(self.local_rank % max(torch.cuda.device_count(), 1))
-                    self.nccl = dist.new_group(backend="nccl")
-                dist.barrier()
-            finally:
-                sys.stdout.flush()
-                os.dup2(saved, 1)
-                os.close(saved)
-            self.dist = dist
+        backend = {"nccl": "rccl", "gloo": "host"}.get(scatter_backend, scatter_backend)
+        self.scatter_backend = backend if (self.world > 1 or force) else "none"
+        self.group = HostGroup(self.rank, self.world) if self.world > 1 else None
+        self.comm = None
+
+    def open_comm(self, ctx):
+        from dpdk_dc_sand_amd.rendezvous import HostGroup
+        from dpdk_dc_sand_amd.shard import ChannelScatter
+        self.comm = ChannelScatter(self.group or HostGroup(0, 1), ctx)
 
     def barrier(self):
-        if self.dist:
-            self.dist.barrier()
+        if self.group:
+            self.group.barrier()
 
     def max(self, v):
-        if not self.dist:
-            return v
-        import torch
-        t = torch.tensor([float(v)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return self.group.allreduce_max(v) if self.group else v
 
     def close(self):
-        if self.dist:
-            self.dist.destroy_process_group()
+        if self.comm:
+            self.comm.close()
+        if self.group:
+            self.group.close()
 
 
 def make_inputs(np, rng, shape, nbuf, unsigned=False):
@@ -148,62 +140,55 @@ def make_inputs(np, rng, shape, nbuf, unsigned=False):
 
 def scatter_inputs(args, dist, shape):
     """The channel scatter: rank 0 holds the full band (B, A, C*N, T, 2, 2) and sends rank r its
-    packed channel slice [C r, C (r+1)).  Returns (per-rank slice, report).  nccl: device tensors over RCCL (the
-    band is generated in rank 0's HBM); gloo: host arrays (rehearsal).  The slice is what this rank's timed hot
-    path then processes."""
+    packed channel slice [C r, C (r+1)).  Returns (per-rank slice, report).  rccl: the band is filled in rank 0's
+    HBM (bf_fill_random) and each slice lands in a device array (libbf bf_channel_scatter over RCCL); host: numpy
+    band, slices through the TCP group (rehearsal).  The slice is what this rank's timed hot path then processes."""
     import numpy as np
-    import torch
 
-    from dpdk_dc_sand_amd.shard import pack_channel_slices
+    from dpdk_dc_sand_amd import _lib, accel
+    from dpdk_dc_sand_amd.shard import pack_channel_slices, scatter_channel_slices
 
     B, A, C, T = shape[:4]
     world, rank = dist.world, dist.rank
     per_rank = int(np.prod(shape))
-    tdt = torch.uint8 if args.unsigned else torch.int8
+    dt = np.uint8 if args.unsigned else np.int8
     report = {"backend": dist.scatter_backend, "bytes_per_rank": per_rank, "ranks": world,
               "band_shape": [B, A, C * world, T, 2, 2]}
-    if dist.scatter_backend == "nccl":
-        dev = torch.device("cuda", torch.cuda.current_device())
-        parts = None
-        if rank == 0:
-            g = torch.Generator(device=dev)
-            g.manual_seed(1)
-            lo, hi = (0, 256) if args.unsigned else (-128, 128)
-            band = torch.randint(lo, hi, (B, A, C * world, T, 2, 2), dtype=tdt, device=dev, generator=g)
-            parts = [band[:, :, r * C:(r + 1) * C].contiguous() for r in range(world)]  # pack: B*A strided runs
-            del band
-        out = torch.empty(shape, dtype=tdt, device=dev)
-        warm = torch.ones(1, device=dev)
-        dist.dist.all_reduce(warm, group=dist.nccl)  # communicator set-up outside the timing
+    if dist.scatter_backend == "rccl":
+        dist.open_comm(args.ctx)
+        band, err = None, None
+        try:
+            if rank == 0:
+                band = accel.DeviceArray(args.ctx, (B, A, C * world, T, 2, 2), dt)
+                _lib.call("bf_fill_random", band.ptr, band.nbytes, 1, args.queue.handle)
+            out = accel.DeviceArray(args.ctx, shape, dt)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if dist.max(1.0 if err else 0.0) > 0:  # agree before any rank posts its ncclRecv
+            raise err or RuntimeError("scatter set-up failed on another rank")
         times = []
         for _ in range(3):
-            torch.cuda.synchronize()
+            args.queue.finish()
             dist.barrier()
             t0 = time.perf_counter()
-            dist.dist.scatter(out, scatter_list=parts, src=0, group=dist.nccl)
-            torch.cuda.synchronize()
+            dist.comm.scatter(band, out, B, A, C, T, args.queue)
+            args.queue.finish()
             times.append(time.perf_counter() - t0)
-        del parts
+        del band
         t = dist.max(min(times))
-        report["collective"] = "RCCL scatter (torch.distributed nccl) over xGMI, device to device"
+        report["collective"] = ("RCCL grouped ncclSend/ncclRecv over xGMI via libbf bf_channel_scatter, device to "
+                                "device (root: one 2-D pack per peer)")
     else:
         full = None
         if rank == 0:
             rng = np.random.default_rng(1)
-            n = B * A * C * world * T * 4
-            full = np.frombuffer(rng.bytes(n), np.uint8 if args.unsigned else np.int8).reshape(
-                B, A, C * world, T, 2, 2)
+            full = np.frombuffer(rng.bytes(B * A * C * world * T * 4), dt).reshape(B, A, C * world, T, 2, 2)
         dist.barrier()
         t0 = time.perf_counter()
-        ttype = torch.from_numpy(np.zeros(1, np.uint8 if args.unsigned else np.int8)).dtype
-        out = torch.empty(shape, dtype=ttype)
-        if rank == 0:
-            dist.dist.scatter(out, scatter_list=[torch.from_numpy(p) for p in pack_channel_slices(full, world)], src=0)
-        else:
-            dist.dist.scatter(out, src=0)
+        out = scatter_channel_slices(full, shape, dt, dist.group)
         t = dist.max(time.perf_counter() - t0)
-        out = out.numpy()
-        report["collective"] = "gloo scatter through host memory (rehearsal backend)"
+        del full, pack_channel_slices
+        report["collective"] = "host memory over the TCP rendezvous group (rehearsal backend)"
     report["seconds"] = round(t, 6)
     report["GBps_per_peer"] = round(per_rank / t / 1e9, 2)
     report["GBps_root_egress"] = round(per_rank * (world - 1) / t / 1e9, 2)
@@ -230,8 +215,8 @@ def delay_model(np, rng, shape):
 
 
 def run_gpu(args, dist, wl, tmpl=None, inputs=None):
-    """Time K launches of the fused operator.  `inputs`: this rank's resident input (a torch device tensor from
-    the RCCL scatter, or a host array), else synthetic host data."""
+    """Time K launches of the fused operator.  `inputs`: this rank's resident input (an accel.DeviceArray from the
+    RCCL scatter, or a host array from the host scatter), else synthetic host data."""
     import numpy as np
 
     from dpdk_dc_sand_amd import accel
@@ -244,25 +229,23 @@ def run_gpu(args, dist, wl, tmpl=None, inputs=None):
     hosts = None
     if inputs is None:
         hosts = make_inputs(np, rng, tmpl.input_shape, args.nbuf, args.unsigned)
+    on_device = isinstance(inputs, accel.DeviceArray)
     for i in range(args.nbuf):
         op = tmpl.instantiate(queue)
-        if inputs is not None and hasattr(inputs, "data_ptr"):
-            # the scattered device tensor itself for buffer 0, a device-side copy for the others
-            src = inputs if i == 0 else inputs.clone()
-            op.bind(inSamples=accel.DeviceArray(args.ctx, tmpl.input_shape, op.slots["inSamples"].dtype,
-                                                ptr=src.data_ptr(), owner=False))
-            op._keep = src
+        if on_device and i == 0:
+            op.bind(inSamples=inputs)  # the scattered slice itself (received in place), no copy
         op.ensure_all_bound()
         if hosts is not None:
             op.buffer("inSamples").set(queue, hosts[i])
-        elif not hasattr(inputs, "data_ptr"):
+        elif on_device:
+            if i > 0:
+                op.buffer("inSamples").copy_region(queue, inputs)  # a device-side copy for the other buffers
+        else:
             op.buffer("inSamples").set(queue, inputs)
         op.buffer("delay_vals").set(queue, d)
         ops.append(op)
     del hosts
-    if inputs is not None and hasattr(inputs, "data_ptr"):
-        import torch
-        torch.cuda.synchronize()  # the clones are on torch's stream
+    queue.finish()
     for i in range(args.warmup):
         ops[i % len(ops)]()
     queue.finish()
@@ -278,6 +261,7 @@ def run_gpu(args, dist, wl, tmpl=None, inputs=None):
         queue.finish()
 
     e0, e1 = accel.Event(), accel.Event()
+    queue.trace_mark(1)  # the timed region's bounds in a profiler trace (tools/kernel_stats.py), outside the timing
     dist.barrier()
     queue.finish()
     t0 = time.perf_counter()
@@ -287,6 +271,7 @@ def run_gpu(args, dist, wl, tmpl=None, inputs=None):
     e1.record(queue)
     queue.finish()
     t_local = time.perf_counter() - t0
+    queue.trace_mark(2)
     dist.barrier()
     kernel_s = e1.time_since(e0) / args.steps
     t_max = dist.max(t_local)
@@ -384,7 +369,12 @@ def cpu_baseline(wl, out_int8, seconds=10.0):
     c = int(min(max(16, c * seconds / max(dt, 1e-3)), wl["C"]))
     dt = once(c)
     rate = A * 2 * c * T * B / dt / 1e9
-    return {"value": round(rate, 4), "unit": "Gsamples/s", "cores": int(threads), "kind": "port",
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - non-Linux
+        affinity = os.cpu_count()
+    return {"value": round(rate, 4), "unit": "Gsamples/s", "cores": int(threads), "blas_threads": int(threads),
+            "host_cpus_in_affinity": int(affinity), "kind": "port",
             "sample": f"{c} of {wl['C']} channels x B={B} x T={T} x A={A} x 2 pols ({dt:.1f} s): oracle.fused_beamform "
                       f"(NumPy reorder + float64-phase coefficients + float32 matmul{' + requantise' if out_int8 else ''}, "
                       f"BLAS threads={threads})"}
@@ -420,6 +410,67 @@ def pmc_traffic(args):
         vals[counter] = sorted(per)[len(per) // 2]
     traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
     return traffic, vals
+
+
+ADC_SAMPLE_RATE, FFT_SIZE = 1712e6, 8192  # MeerKAT L-band (BeamformerParameters.h:15-16)
+
+
+def realtime(wl, n_gpus, value_gsps):
+    """Real-time factor against MeerKAT ingest, as the reference's harness reports GPU utilisation
+    (BeamformerCoefficientTest.cu:422-465: kernel time / the wall time the processed spectra represent): the band
+    needs A * 2 pols * C * N channels * (ADC rate / FFT size) samples/s; `gpus_per_band` is that need over this
+    run's whole-job rate x N (the reference's "GPUs required")."""
+    spectra_per_s = ADC_SAMPLE_RATE / FFT_SIZE
+    need = wl["A"] * 2 * wl["C"] * n_gpus * spectra_per_s / 1e9
+    return {"ingest_need_Gsamples_s": round(need, 2), "realtime_factor": round(value_gsps / need, 2),
+            "gpus_per_band": round(need / value_gsps * n_gpus, 4),
+            "basis": f"{wl['A']} ants x 2 pols x {wl['C'] * n_gpus} channels x {spectra_per_s:.1f} spectra/s "
+                     "(ADC 1712 MHz / FFT 8192, BeamformerParameters.h:15-16; BeamformerCoefficientTest.cu:422-465)"}
+
+
+def rocprof_check(args, n_secondary):
+    """The same bench (headline + secondaries, no PMC / CPU baseline / ceiling) re-run as a child under
+    `rocprofv3 --kernel-trace`; each timed region (bracketed by bf_trace_mark dispatches) summarised per kernel by
+    tools/kernel_stats.py.  Returns ([region stats], the child's own JSON line) -- the child's events and its
+    profiled kernel durations come from the same process, so they must agree."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_stats
+    exe = "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, None, "rocprofv3 not found"
+    out = args.prof_out or tempfile.mkdtemp(prefix="bfprof_", dir=os.environ.get("TMPDIR", "/tmp"))
+    os.makedirs(out, exist_ok=True)
+    cmd = [exe, "--kernel-trace", "--output-format", "csv", "-d", out, "-o", "bench", "--", sys.executable,
+           os.path.abspath(__file__), "--prof-child", "--workload", args.workload, "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--settle-ms", str(args.settle_ms), "--output", args.output,
+           "--int8-contract", args.int8_contract, "--no-pmc", "--no-cpu-baseline", "--no-ceiling"]
+    cmd += (["--unsigned"] if args.unsigned else []) + (["--no-secondary"] if n_secondary == 0 else [])
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
+    files = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
+    if r.returncode != 0 or not files:
+        return None, None, f"rocprofv3 failed rc={r.returncode}: {r.stderr[-300:]}"
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    child = json.loads(lines[-1]) if lines else None
+    regions = kernel_stats.region_stats(files[0])
+    kernel_stats.write_csv(regions, os.path.join(out, "timed_kernel_stats.csv"))
+    if child is not None:
+        with open(os.path.join(out, "prof_bench.json"), "w") as f:
+            f.write(json.dumps(child) + "\n")
+    return regions, child, None
+
+
+def rocprof_entry(regions, i, kernel, alg_bytes):
+    """The timed dispatches of `kernel` in region i: count, average / median duration, roofline fraction."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_stats
+    if regions is None or i >= len(regions):
+        return None
+    name, s = kernel_stats.dominant(regions[i], "::" + kernel + "<")
+    if s is None:
+        return {"error": f"no {kernel} dispatches in timed region {i}"}
+    return {"kernel_instance": name, "timed_dispatches": s["Calls"], "avg_us": round(s["AverageNs"] / 1e3, 2),
+            "median_us": round(s["MedianNs"] / 1e3, 2), "max_us": round(s["MaxNs"] / 1e3, 2),
+            "frac": round(alg_bytes / (s["AverageNs"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def compute_desc(out_int8, int8_contract):
@@ -465,11 +516,12 @@ def secondary(args, dist, workload, out_int8, int8_contract="q14"):
            "output": ("int8" + ("" if int8_contract == "q14" else " (requantised from float32 beams)"))
            if out_int8 else "float32",
            "kernel": kernel_name(wl, out_int8, int8_contract),
-           "value": round(r["samples_per_step"] * args.steps / r["t_max"] / 1e9, 2), "unit": "Gsamples/s",
+           "value": round(r["samples_per_step"] * args.steps * dist.world / r["t_max"] / 1e9, 2),
+           "unit": "Gsamples/s", "n_gpus": dist.world,
            "roofline_frac": round(r["alg_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
            "read_frac": round(r["read_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
            "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"]}
-    if not args.no_ceiling:
+    if not args.no_ceiling and dist.world == 1:
         ceil = stream_ceiling(args, r["read_bytes"], int(r["alg_bytes"] - r["read_bytes"]))
         if ceil:
             out["ceiling"] = ceil
@@ -496,7 +548,7 @@ def main():
     inputs = None
     if dist.scatter_backend != "none":
         # the scatter is reported beside the hot path, not part of it: if the collective raises (on every rank),
-        # the ranks agree over gloo and generate their shards in place, so the timed line is still produced
+        # the ranks agree over the TCP group and generate their shards in place, so the timed line is still produced
         err = None
         try:
             inputs, scatter = scatter_inputs(args, dist, tmpl.input_shape)
@@ -532,9 +584,10 @@ def main():
         "mfma": mfma_util(wl, args.out_int8, args.int8_contract, r["kernel_s"]),
         "scatter": scatter or {"backend": None, "note": "no scatter: single rank, or --scatter-backend none "
                                                         "(each rank generates its shard in place)"},
+        "realtime": realtime(wl, dist.world, value),
         "cpu_baseline": None,
     }
-    if dist.rank == 0 and dist.world == 1 and args.out_int8 and args.int8_contract == "q14":
+    if dist.rank == 0 and dist.world == 1 and args.out_int8 and args.int8_contract == "q14" and not args.prof_child:
         line["int8_contract_check"] = contract_check(args, dist, wl, r)
     r.pop("ops")
     if dist.rank == 0 and dist.world == 1 and not args.no_ceiling:
@@ -542,10 +595,14 @@ def main():
         if ceil:
             line["ceiling"] = ceil
             line["roofline"]["frac_of_ceiling"] = round(ceil["us"] / line["roofline"]["avg_launch_us"], 4)
-    if dist.rank == 0 and dist.world == 1 and not args.no_secondary and args.workload == "cfg3":
+    if not args.no_secondary and args.workload == "cfg3":
+        # every rank runs the secondaries (each is timed between barriers, max over ranks); at N > 1 config 4
+        # channel-sharded: 4096 channels per rank of the 32768-channel band (BASELINE configs[3] at N = 8)
         line["secondary"] = []
         cases = [("cfg2", args.out_int8, "q14"), ("cfg3", not args.out_int8, "q14"), ("cfg3", True, "f32"),
                  ("cfg4", True, "q14"), ("cfg4", False, "q14")]
+        if dist.world > 1:
+            cases = [("cfg4", True, "q14"), ("cfg4", False, "q14")]
         for workload, out_int8, contract in cases:
             if (workload, out_int8, contract if out_int8 else "q14") == (args.workload, args.out_int8,
                                                                           args.int8_contract if args.out_int8 else "q14"):
@@ -554,6 +611,26 @@ def main():
                 line["secondary"].append(secondary(args, dist, workload, out_int8, contract))
             except Exception as e:  # secondary lines are informational
                 line["secondary"].append({"workload": workload, "error": str(e)[:200]})
+    if dist.rank == 0 and dist.world == 1 and not (args.no_rocprof or args.prof_child):
+        secs = [s for s in line.get("secondary", []) if "error" not in s]
+        try:
+            regions, child, err = rocprof_check(args, len(secs))
+        except Exception as e:  # informational: the live event timing above is the measurement
+            regions, child, err = None, None, f"{type(e).__name__}: {str(e)[:200]}"
+        if err:
+            line["roofline"]["rocprof"] = {"error": err}
+        else:
+            ent = rocprof_entry(regions, 0, line["roofline"]["kernel"], r["alg_bytes"]) or {}
+            ent.update({"profiled_run_ms_per_step": child.get("ms_per_step") if child else None,
+                        "profiled_run_event_avg_us": child["roofline"]["avg_launch_us"] if child else None,
+                        "source": "rocprofv3 --kernel-trace re-run of this bench (same args, child process): the "
+                                  "timed dispatches only, between the two bf_trace_mark dispatches of each timed "
+                                  "region (tools/kernel_stats.py)"})
+            line["roofline"]["rocprof"] = ent
+            for i, s in enumerate(secs):
+                e = rocprof_entry(regions, i + 1, s["kernel"], s["alg_bytes_per_launch"])
+                if e:
+                    s["rocprof"] = e
     if dist.rank == 0 and dist.world == 1 and not args.no_pmc:
         try:
             traffic, info = pmc_traffic(args)

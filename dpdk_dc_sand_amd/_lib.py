@@ -44,6 +44,7 @@ PROTOTYPES = {
     "bf_event_record": (c_int, [c_void_p, c_void_p]),
     "bf_event_synchronize": (c_int, [c_void_p]),
     "bf_event_elapsed_ms": (c_int, [P_float, c_void_p, c_void_p]),
+    "bf_trace_mark": (c_int, [c_int, c_void_p]),
     "bf_coeff_gen": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_double,
                              c_void_p]),
     "bf_coeff_gen_time": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -69,13 +70,19 @@ PROTOTYPES = {
     "bf_pipeline_stage_ms": (c_int, [c_void_p, c_longlong, P_float, P_float, P_float]),
     "bf_requant": (c_int, [c_void_p, c_void_p, c_size_t, c_float, c_void_p]),
     "bf_fused_algorithmic_bytes": (c_double, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "bf_comm_unique_id": (c_int, [c_void_p, c_size_t]),
+    "bf_comm_create": (c_int, [P_void, c_void_p, c_size_t, c_int, c_int]),
+    "bf_comm_destroy": (c_int, [c_void_p]),
+    "bf_comm_allreduce_max": (c_int, [c_void_p, ctypes.POINTER(c_double)]),
+    "bf_channel_scatter": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "bf_fill_random": (c_int, [c_void_p, c_size_t, ctypes.c_ulonglong, c_void_p]),
 }
 
 
 # bf_beamform_fused flags (include/bf.h)
 FUSED_SIGNED, FUSED_OUT_INT8, FUSED_EXACT_COEFF, FUSED_INT8_VIA_F32 = 1, 2, 4, 8
 # kernel-path / workgroup-order overrides (tests and measurement; every path computes the same contract)
-FUSED_PATH = {"auto": 0, "item": 0x100, "pipe": 0x200, "generic": 0x300, "wide": 0x400, "wide16": 0x500, "staged": 0x600}
+FUSED_PATH = {"auto": 0, "item": 0x100, "generic": 0x300, "wide": 0x400, "wide16": 0x500}
 FUSED_ORDER = {"auto": 0, "channel": 0x1000, "xcd": 0x2000}
 
 

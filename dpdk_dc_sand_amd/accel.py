@@ -108,6 +108,11 @@ class CommandQueue:
     def enqueue_marker(self):
         return Event(self)
 
+    def trace_mark(self, tag=0):
+        """One empty `bf_trace_mark_kernel` dispatch on this stream: delimits a region of a profiler's kernel trace
+        (tools/kernel_stats.py)."""
+        _lib.call("bf_trace_mark", int(tag), self.handle)
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h:

@@ -39,7 +39,7 @@ class FusedBeamformerTemplate:
     beam_weights: carry a per-(beam, input) real weight table (slot beamWeights, set with set_beam_weights).
     int8_contract: with out_int8, "q14" (default: the integer contract, Q14 coefficients and exact int32 sums on the
         integer MFMA path) or "f32" (requantised float32 beams: the reference's float32 coefficient arithmetic).
-    kernel_path, workgroup_order: force a kernel path ("auto", "item", "pipe", "generic", "wide", "wide16", "staged") or
+    kernel_path, workgroup_order: force a kernel path ("auto", "item", "generic", "wide", "wide16") or
         workgroup order ("auto", "channel", "xcd") -- tests and measurement; every path computes the same contract.
     """
 

@@ -560,15 +560,11 @@ int launch_persist(const uint8_t* x, const float* w, float* y, long long bpc, in
              "bf_beamform: shape does not fit the persistent table kernel");
   const int xcd = nslabs > 1;
   const long long nitems = xcd ? (bpc + 7) / 8 * 8 * nslabs : bpc * nslabs;
-  static int n_cu = 0;
-  if (n_cu == 0) {
-    int dev = 0, n = 0;
-    BF_HIP(hipGetDevice(&dev));
-    BF_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
-    n_cu = n > 0 ? n : 256;
-  }
-  const long long grid = std::min<long long>(nitems, 2LL * n_cu / 8 * 8);  // a multiple of 8 (item XCD = workgroup's)
-  BF_REQUIRE(grid > 0 && grid % 8 == 0, "bf_beamform: persistent grid");
+  // two workgroups per CU; with the XCD item order the grid is a multiple of 8 (an item's XCD is its workgroup's:
+  // nitems is then a multiple of 8 too), otherwise any size
+  const int n_cu = cu_count();
+  const long long grid = std::min<long long>(nitems, xcd ? 2LL * n_cu / 8 * 8 : 2LL * n_cu);
+  BF_REQUIRE(grid > 0 && (!xcd || grid % 8 == 0), "bf_beamform: persistent grid");
   hipLaunchKernelGGL((beamform_table_persist_kernel<Signed, NTS, R, UPT, Mode>), dim3(static_cast<unsigned>(grid)),
                      dim3(kThreads), lds, st, x, w, y, NB, A, M, S, NT, nslabs, bpc, xcd, nitems);
   BF_LAUNCHED("beamform_table_persist_kernel");

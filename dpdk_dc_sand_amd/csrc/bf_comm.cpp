@@ -1,0 +1,219 @@
+// Multi-GPU channel scatter over RCCL: the only collective of the channel-sharded beamformer.
+//
+// The reference has no multi-GPU path: each X-engine (xeng_id) owns a contiguous block of channels whose absolute
+// index is c + C * xeng_id (beamformer/beamforming/coeff_generator.py:49-53), and its one multi-device pattern is a
+// host thread per device (utilities/pcie_bandwidth_tests/main.cpp:193-224, cudaPcieRateTest.cpp:9).  Here one
+// process drives one GPU (rank r = X-engine r) and the root hands every rank its channel slice of a full-band
+// voltage cube once, device to device over xGMI:
+//   root: each peer's slice (B * A strided runs of C*T*4 bytes in the (B, A, C*N, T, 2, 2) band) is packed into a
+//         contiguous staging block by one 2-D copy (the root's own slice straight into its output), then one
+//         grouped ncclSend per peer -- each peer's bytes travel on their own xGMI link at once;
+//   peers: one ncclRecv of the whole slice into the (B, A, C, T, 2, 2) input buffer of the fused beamformer.
+// Everything is ordered on the caller's stream; nothing on the beamforming hot path touches RCCL.
+//
+// RCCL is loaded at first use (dlopen of /opt/rocm's librccl.so.1, the ROCm release libbf is built against), so a
+// single-GPU user of libbf never maps it.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+
+#include "bf_common.hpp"
+
+namespace {
+
+struct Rccl {
+  void* handle = nullptr;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  std::string load_error;
+};
+
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+      r.handle = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (r.handle) break;
+    }
+    if (!r.handle) {
+      const char* e = dlerror();
+      r.load_error = e ? e : "dlopen(librccl.so.1) failed";
+      return;
+    }
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(r.handle, name));
+      if (!fn && r.load_error.empty()) r.load_error = std::string("librccl lacks ") + name;
+    };
+    sym(r.get_unique_id, "ncclGetUniqueId");
+    sym(r.comm_init_rank, "ncclCommInitRank");
+    sym(r.comm_destroy, "ncclCommDestroy");
+    sym(r.group_start, "ncclGroupStart");
+    sym(r.group_end, "ncclGroupEnd");
+    sym(r.send, "ncclSend");
+    sym(r.recv, "ncclRecv");
+    sym(r.all_reduce, "ncclAllReduce");
+    sym(r.error_string, "ncclGetErrorString");
+  });
+  return r;
+}
+
+int rccl_fail(ncclResult_t e, const char* what) {
+  const Rccl& r = rccl();
+  bf::set_error("%s: %s (%d)", what, r.error_string ? r.error_string(e) : "RCCL error", static_cast<int>(e));
+  return BF_ERR_COMM;
+}
+
+#define BF_RCCL(call)                                              \
+  do {                                                             \
+    ncclResult_t bf_r_ = (call);                                   \
+    if (bf_r_ != ncclSuccess) return rccl_fail(bf_r_, #call);      \
+  } while (0)
+
+#define BF_RCCL_LOADED()                                                                        \
+  do {                                                                                          \
+    if (!rccl().load_error.empty()) {                                                           \
+      ::bf::set_error("RCCL unavailable: %s", rccl().load_error.c_str());                       \
+      return BF_ERR_COMM;                                                                       \
+    }                                                                                           \
+  } while (0)
+
+}  // namespace
+
+struct bf_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+  void* staging = nullptr;  // root: (nranks - 1) packed peer slices
+  size_t staging_bytes = 0;
+  double* d_scalar = nullptr;  // allreduce scratch
+  hipStream_t stream = nullptr;
+};
+
+extern "C" {
+
+int bf_comm_unique_id(void* id, size_t len) {
+  BF_REQUIRE(id != nullptr && len >= BF_COMM_ID_BYTES, "bf_comm_unique_id: need a %d-byte buffer",
+             BF_COMM_ID_BYTES);
+  static_assert(sizeof(ncclUniqueId) == BF_COMM_ID_BYTES, "ncclUniqueId size");
+  BF_RCCL_LOADED();
+  ncclUniqueId u;
+  BF_RCCL(rccl().get_unique_id(&u));
+  std::memcpy(id, &u, sizeof(u));
+  bf::clear_error();
+  return BF_OK;
+}
+
+int bf_comm_create(bf_comm** out, const void* id, size_t len, int nranks, int rank) {
+  BF_REQUIRE(out != nullptr && id != nullptr, "bf_comm_create: null pointer");
+  *out = nullptr;
+  BF_REQUIRE(len == BF_COMM_ID_BYTES, "bf_comm_create: the unique id has %d bytes", BF_COMM_ID_BYTES);
+  BF_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bf_comm_create: rank %d of %d", rank, nranks);
+  BF_RCCL_LOADED();
+  auto* c = new bf_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  hipError_t e = hipGetDevice(&c->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_scalar), sizeof(double));
+  if (e != hipSuccess) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return bf::hip_fail(e, "bf_comm_create");
+  }
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  const ncclResult_t r = rccl().comm_init_rank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    (void)hipFree(c->d_scalar);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return rccl_fail(r, "ncclCommInitRank");
+  }
+  *out = c;
+  bf::clear_error();
+  return BF_OK;
+}
+
+int bf_comm_destroy(bf_comm* c) {
+  if (!c) return BF_OK;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  const ncclResult_t r = c->comm ? rccl().comm_destroy(c->comm) : ncclSuccess;
+  if (c->staging) (void)hipFree(c->staging);
+  (void)hipFree(c->d_scalar);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  if (prev >= 0) (void)hipSetDevice(prev);
+  if (r != ncclSuccess) return rccl_fail(r, "ncclCommDestroy");
+  return BF_OK;
+}
+
+int bf_comm_allreduce_max(bf_comm* c, double* value) {
+  BF_REQUIRE(c != nullptr && value != nullptr, "bf_comm_allreduce_max: null pointer");
+  BF_HIP(hipMemcpyAsync(c->d_scalar, value, sizeof(double), hipMemcpyHostToDevice, c->stream));
+  BF_RCCL(rccl().all_reduce(c->d_scalar, c->d_scalar, 1, ncclFloat64, ncclMax, c->comm, c->stream));
+  BF_HIP(hipMemcpyAsync(value, c->d_scalar, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  BF_HIP(hipStreamSynchronize(c->stream));
+  return BF_OK;
+}
+
+int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, int A, int C, int T, int root,
+                       void* stream) {
+  BF_REQUIRE(c != nullptr && slice != nullptr, "bf_channel_scatter: null pointer");
+  BF_REQUIRE(B > 0 && A > 0 && C > 0 && T > 0, "bf_channel_scatter: bad shape B=%d A=%d C=%d T=%d", B, A, C, T);
+  BF_REQUIRE(root >= 0 && root < c->nranks, "bf_channel_scatter: root %d of %d ranks", root, c->nranks);
+  BF_REQUIRE(c->rank != root || band != nullptr, "bf_channel_scatter: the root needs the band");
+  hipStream_t st = bf::as_stream(stream);
+  const size_t run = static_cast<size_t>(C) * T * 4;            // one (b, a) channel run of a slice
+  const size_t pitch = run * static_cast<size_t>(c->nranks);    // the band's (b, a) row
+  const size_t rows = static_cast<size_t>(B) * A;
+  const size_t slice_bytes = run * rows;
+  if (c->rank == root) {
+    const size_t need = slice_bytes * static_cast<size_t>(c->nranks - 1);
+    if (need > c->staging_bytes) {
+      if (c->staging) {
+        BF_HIP(hipStreamSynchronize(st));
+        BF_HIP(hipFree(c->staging));
+        c->staging = nullptr;
+        c->staging_bytes = 0;
+      }
+      BF_HIP(hipMalloc(&c->staging, need));
+      c->staging_bytes = need;
+    }
+    uint8_t* stg = static_cast<uint8_t*>(c->staging);
+    for (int r = 0, k = 0; r < c->nranks; ++r) {
+      uint8_t* dst = r == root ? slice : stg + slice_bytes * static_cast<size_t>(k++);
+      BF_HIP(hipMemcpy2DAsync(dst, run, band + run * static_cast<size_t>(r), pitch, run, rows,
+                              hipMemcpyDeviceToDevice, st));
+    }
+    if (c->nranks == 1) return BF_OK;
+    BF_RCCL(rccl().group_start());
+    for (int r = 0, k = 0; r < c->nranks; ++r) {
+      if (r == root) continue;
+      const ncclResult_t e = rccl().send(stg + slice_bytes * static_cast<size_t>(k++), slice_bytes, ncclUint8, r,
+                                         c->comm, st);
+      if (e != ncclSuccess) {
+        (void)rccl().group_end();
+        return rccl_fail(e, "ncclSend");
+      }
+    }
+    BF_RCCL(rccl().group_end());
+  } else {
+    BF_RCCL(rccl().recv(slice, slice_bytes, ncclUint8, root, c->comm, st));
+  }
+  bf::clear_error();
+  return BF_OK;
+}
+
+}  // extern "C"

@@ -61,4 +61,30 @@ inline const char* diag_env(const char* name) {
 
 constexpr int kSamplesPerBlock = 16;  // matrix_multiply.py:76 (128 // 8)
 
+// Launch flags of bf_beamform_fused* and bf_pipeline_create (include/bf.h): only known bits, a defined kernel
+// path, a defined workgroup order.  Returns nullptr when valid, else what is wrong.
+inline const char* fused_flags_error(int flags) {
+  if (flags & ~(BF_FUSED_SIGNED | BF_FUSED_OUT_INT8 | BF_FUSED_EXACT_COEFF | BF_FUSED_INT8_VIA_F32 |
+                BF_FUSED_PATH_MASK | BF_FUSED_ORDER_MASK))
+    return "unknown flags";
+  const int path = flags & BF_FUSED_PATH_MASK;
+  if (path != 0 && path != BF_FUSED_PATH_ITEM && path != BF_FUSED_PATH_GENERIC && path != BF_FUSED_PATH_WIDE &&
+      path != BF_FUSED_PATH_WIDE16)
+    return "unknown kernel path";
+  if ((flags & BF_FUSED_ORDER_MASK) == BF_FUSED_ORDER_MASK) return "unknown workgroup order";
+  return nullptr;
+}
+
+// The Q14 integer path's int32 beam sums: |y| <= A * max|x| * (sqrt(2) * rne(max|g| * 2^14) + 1) must stay below
+// 2^31 (max|x| = 128 for int8 samples, 255 for uint8), and the high limb of rne(g * 2^14) must stay int8
+// (|g| <= 1.992).  The oracle sums in int64; beyond the bound the int32 accumulators would wrap.
+inline bool q14_sum_bound_ok(int A, bool sample_signed, double max_gain) {
+  if (__builtin_rint(max_gain * 16384.0) > 32639.0) return false;
+  return static_cast<double>(A) * (sample_signed ? 128 : 255) * (1.4142135623730951 * 16384.0 * max_gain + 1.0) <
+         2147483648.0;
+}
+
+// Compute units of the current device (cached per device index; sizes persistent grids only).
+int cu_count();
+
 }  // namespace bf

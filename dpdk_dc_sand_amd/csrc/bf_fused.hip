@@ -299,114 +299,6 @@ __device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, in
                                      int wave, bool tv, const f32x4 (&acc)[4][NTS]);
 
 // ---------------------------------------------------------------------------------------------------------
-// Persistent, software-pipelined kernel (A <= 64, T <= 256: one load group, one 64-sample chunk per wave).
-// grid = resident workgroups (2 per CU); workgroup g walks items g, g + grid, ... (item = (slab, b, c), c
-// fastest so concurrently running workgroups read adjacent 1 KiB antenna runs).  Per half-iteration it
-//   1. issues the NEXT item's voltage loads into the other register set,
-//   2. regenerates the NEXT item's coefficients into the other LDS buffer (VALU, under the loads' latency),
-//   3. contracts the CURRENT item on MFMA (one pol at a time) and stores its beams,
-//   4. barriers (LDS hand-over),
-// so HBM reads, coefficient VALU, MFMA and the store stream of different items overlap inside every wave.
-template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
-__global__ __launch_bounds__(kThreads, 2) void beamform_fused_pipe_kernel(FusedArgs P) {
-  extern __shared__ __attribute__((aligned(16))) half8 lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 4, tl = lane & 15;
-  const int T4 = P.T >> 2;
-  const int tq = wave * 16 + tl;
-  const bool tv = tq < T4;
-  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
-  const int coef_elems = P.S * NTS * 2 * 64;  // half8 per LDS coefficient buffer
-  const int n_items = P.nslabs * P.B * P.C;
-
-  auto split = [&](int item, int& slab, int& b, int& c) {
-    c = item % P.C;
-    const int r = item / P.C;
-    b = r % P.B;
-    slab = r / P.B;
-  };
-  auto prefetch = [&](int item, uint32_t (&d)[kGroup][4][4], half8* buf) {
-    int slab, b, c;
-    split(item, slab, b, c);
-    const int tau0 = slab * NTS;
-    const int nts = Full ? NTS : min(NTS, P.NT - tau0);
-    CoefPrefetch<NTS> cp;
-    if constexpr (!(Mode & kSkipCoef)) load_delays<NTS>(cp, P, c, tau0, nts, tid);  // 1. delay model (oldest)
-    __builtin_amdgcn_sched_barrier(0);  // keep the issue order: waiting for the delays must not drain the voltages
-    if constexpr (!(Mode & kSkipLoad)) {                                             // 2. voltages
-      const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
-      load_group(base, ant_stride, tq, T4, 0, P.A, h, d);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    make_coefs<Exact, Mode, NTS>(reinterpret_cast<_Float16*>(buf), cp, P, b, c, tau0, nts, tid);  // 3. under them
-  };
-  auto run = [&](int item, uint32_t (&d)[kGroup][4][4], const half8* buf) {
-    int slab, b, c;
-    split(item, slab, b, c);
-    flip_group<Signed>(d);
-    const int tau0 = slab * NTS;
-    const int nts = Full ? NTS : min(NTS, P.NT - tau0);
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      f32x4 acc[4][NTS];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int tau = 0; tau < NTS; ++tau) acc[i][tau] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (Mode & kSkipMfma) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i][0][q] = __builtin_bit_cast(float, d[q][p + 1][i] ^ d[q][p][i]);
-      } else {
-        contract_pol<Signed, NTS, Full>(buf, 0, P.S, nts, lane, p, d, acc);
-      }
-      if constexpr (Mode & kSkipStore) {
-        float sum = 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int tau = 0; tau < NTS; ++tau) sum += acc[i][tau][0] + acc[i][tau][1] + acc[i][tau][2] + acc[i][tau][3];
-        if (sum == 1234.5f) reinterpret_cast<float*>(P.y)[tid] = sum;  // keeps the work alive
-      } else {
-        if constexpr (OutI8 && Full)
-          store_f32acc_i8_rows<NTS>(P, b, c, p, tau0, tq, h, lane, wave, tv, acc);
-        else if (tv)
-          store_pol<OutI8, NTS, Full>(P, b, c, p, tau0, nts, tq, h, acc);
-      }
-    }
-  };
-
-  uint32_t dA[kGroup][4][4], dB[kGroup][4][4];
-  if constexpr (Mode & kSkipLoad) {
-#pragma unroll
-    for (int ss = 0; ss < kGroup; ++ss)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dA[ss][q][j] = dB[ss][q][j] = static_cast<uint32_t>(tid * 0x01010101u + ss + q + j);
-  }
-  half8* bufA = lds;
-  half8* bufB = lds + coef_elems;
-  int item = blockIdx.x;
-  if (item < n_items) prefetch(item, dA, bufA);
-  __syncthreads();
-  while (item < n_items) {
-    int next = item + gridDim.x;
-    if (next < n_items) prefetch(next, dB, bufB);
-    run(item, dA, bufA);
-    __syncthreads();
-    item = next;
-    if (item >= n_items) break;
-    next = item + gridDim.x;
-    if (next < n_items) prefetch(next, dA, bufA);
-    run(item, dB, bufB);
-    __syncthreads();
-    item = next;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------------------
 // Single-item kernel (A <= 64, T <= 256): grid = items, one (slab, b, c) per workgroup, one register set.
 // Issue order delay model -> voltages (16 x 16 B per lane, all in flight) -> coefficient math under them ->
 // barrier -> per pol: MFMA contraction + stores.  Memory/compute overlap comes from the 3+ workgroups a CU holds
@@ -1227,9 +1119,8 @@ int launch_i8(FusedArgs P, hipStream_t st) {
   const int S8 = (2 * P.A + 63) / 64;
   const int choice = fused_kernel_choice(P);
   const bool small = S8 <= 2 && P.T <= 256;
-  if (choice == BF_FUSED_PATH_STAGED && i8_wide_lc_fits(P)) return launch_i8_wide_lc<Signed>(P, st);
   if ((choice == BF_FUSED_PATH_WIDE || (choice == 0 && !small)) && i8_w32_fits(P)) return launch_i8_w32<Signed>(P, st);
-  if ((choice == BF_FUSED_PATH_WIDE || choice == BF_FUSED_PATH_WIDE16 || choice == BF_FUSED_PATH_STAGED ||
+  if ((choice == BF_FUSED_PATH_WIDE || choice == BF_FUSED_PATH_WIDE16 ||
        (choice == 0 && !small)) && i8_wide_fits(P))
     return launch_i8_wide<Signed>(P, st);
   if (small && choice != BF_FUSED_PATH_GENERIC) {
@@ -1257,25 +1148,6 @@ int launch_i8(FusedArgs P, hipStream_t st) {
                        lds_bytes(1), st, P);
   }
   BF_LAUNCHED("beamform_fused_i8_kernel");
-}
-
-template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0>
-int launch_pipe(FusedArgs P, hipStream_t st) {
-  P.nslabs = (P.NT + NTS - 1) / NTS;
-  const size_t lds = 2 * coef_lds_bytes(P.S, NTS);
-  auto kern = beamform_fused_pipe_kernel<Signed, OutI8, NTS, Exact, Full, Mode>;
-  int dev = 0, cus = 256, per_cu = 2;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                              hipSuccess)
-    cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds) != hipSuccess) per_cu = 2;
-  per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
-  const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
-  BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many (batch, channel) items");
-  long long grid = static_cast<long long>(cus) * per_cu;
-  if (grid > n_items) grid = n_items;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), lds, st, P);
-  BF_LAUNCHED("beamform_fused_pipe_kernel");
 }
 
 template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0, int Occ = 1>
@@ -1316,14 +1188,6 @@ int dispatch(FusedArgs P, hipStream_t st) {
   }
   if (small && choice != BF_FUSED_PATH_GENERIC) {
     const int M2 = 2 * P.M;
-    if (choice == BF_FUSED_PATH_PIPE) {
-      if (P.NT >= 2) {
-        if (M2 % 32 == 0) return launch_pipe<Signed, OutI8, 2, Exact, true>(P, st);
-        return launch_pipe<Signed, OutI8, 2, Exact, false>(P, st);
-      }
-      if (M2 == 16) return launch_pipe<Signed, OutI8, 1, Exact, true>(P, st);
-      return launch_pipe<Signed, OutI8, 1, Exact, false>(P, st);
-    }
     if (P.NT >= 2) {
       if (M2 % 32 == 0) return launch_item<Signed, OutI8, 2, Exact, true>(P, st);
       return launch_item<Signed, OutI8, 2, Exact, false>(P, st);
@@ -1357,12 +1221,8 @@ extern "C" int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay
   BF_REQUIRE(T % bf::kSamplesPerBlock == 0, "bf_beamform_fused: n_samples_per_channel=%d must be a multiple of 16", T);
   BF_REQUIRE(delay_channels == 1 || delay_channels == C, "bf_beamform_fused: delay_channels must be 1 or C");
   BF_REQUIRE(sample_period > 0.0, "bf_beamform_fused: sample_period must be > 0");
-  BF_REQUIRE((flags & ~(BF_FUSED_SIGNED | BF_FUSED_OUT_INT8 | BF_FUSED_EXACT_COEFF | BF_FUSED_INT8_VIA_F32 |
-                         BF_FUSED_PATH_MASK | BF_FUSED_ORDER_MASK)) == 0,
-             "bf_beamform_fused: unknown flags 0x%x", flags);
-  BF_REQUIRE((flags & BF_FUSED_PATH_MASK) <= BF_FUSED_PATH_STAGED, "bf_beamform_fused: unknown kernel path 0x%x",
-             flags & BF_FUSED_PATH_MASK);
-  BF_REQUIRE((flags & BF_FUSED_ORDER_MASK) != BF_FUSED_ORDER_MASK, "bf_beamform_fused: unknown workgroup order");
+  const char* ferr = bf::fused_flags_error(flags);
+  BF_REQUIRE(ferr == nullptr, "bf_beamform_fused: %s (flags 0x%x)", ferr, flags);
   BF_REQUIRE((reinterpret_cast<uintptr_t>(raw) & 15) == 0 && (reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 &&
                  (reinterpret_cast<uintptr_t>(y) & 15) == 0,
              "bf_beamform_fused: misaligned buffer");
@@ -1582,7 +1442,8 @@ extern "C" int bf_diag_stream(const void* in, void* out, size_t in_bytes, size_t
   BF_LAUNCHED("stream_kernel");
 }
 
-// Ablation of the pipelined kernel (signed input, f32 output, fast coefficients, full tiles): mode = kSkip* bits.
+// Ablations of the item kernels (signed input, full tiles): mode 32 + kSkip* bits = the float item kernel (f32 beams,
+// fast coefficients), 512 + bits = the integer item kernel.
 extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void* y, int B, int C, int T, int A, int M,
                              int Ctot, double ts, void* stream) {
   bf::FusedArgs P{};
@@ -1603,7 +1464,7 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
   P.batch_dt = 1e-3;
   P.out_scale = 1.0f;
   hipStream_t st = bf::as_stream(stream);
-  BF_REQUIRE(P.S <= bf::kGroup && T <= 256 && (2 * M) % 32 == 0, "diag: pipelined full-tile shapes only");
+  BF_REQUIRE(P.S <= bf::kGroup && T <= 256 && (2 * M) % 32 == 0, "diag: item-kernel full-tile shapes only");
   if (mode >= 512) {  // integer (int8-output) item kernel
     P.out_scale = 1.0f / 64;
     switch (mode - 512) {
@@ -1666,19 +1527,7 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       default: bf::set_error("bad mode"); return BF_ERR_ARG;
     }
   }
-  switch (mode) {
-    case 0: return bf::launch_pipe<true, false, 2, false, true, 0>(P, st);
-    case 1: return bf::launch_pipe<true, false, 2, false, true, 1>(P, st);
-    case 2: return bf::launch_pipe<true, false, 2, false, true, 2>(P, st);
-    case 3: return bf::launch_pipe<true, false, 2, false, true, 3>(P, st);
-    case 4: return bf::launch_pipe<true, false, 2, false, true, 4>(P, st);
-    case 5: return bf::launch_pipe<true, false, 2, false, true, 5>(P, st);
-    case 7: return bf::launch_pipe<true, false, 2, false, true, 7>(P, st);
-    case 8: return bf::launch_pipe<true, false, 2, false, true, 8>(P, st);
-    case 9: return bf::launch_pipe<true, false, 2, false, true, 9>(P, st);
-    case 11: return bf::launch_pipe<true, false, 2, false, true, 11>(P, st);
-    case 16: return bf::launch_pipe<true, false, 2, true, true, 0>(P, st);  // exact coefficients
-    default: bf::set_error("bad mode"); return BF_ERR_ARG;
-  }
+  bf::set_error("bad mode");
+  return BF_ERR_ARG;
 }
 #endif  // BF_DIAG

@@ -90,17 +90,13 @@ __device__ __forceinline__ void lds_barrier() {
 inline int fused_kernel_choice(const FusedArgs& P) { return P.path; }
 
 // Integer wide kernels: int8 beams for many antennas x beams.  bf_wide_i8.hip: a workgroup per 32-beam slab (the
-// default, BF_FUSED_PATH_WIDE) or per 16-beam slab (BF_FUSED_PATH_WIDE16); bf_wide_i8lc.hip: loader/consumer waves
-// of a persistent workgroup (A in [32, 256], M <= 64: BF_FUSED_PATH_STAGED).
+// default, BF_FUSED_PATH_WIDE) or per 16-beam slab (BF_FUSED_PATH_WIDE16).
 bool i8_wide_fits(const FusedArgs& P);
 template <bool Signed>
 int launch_i8_wide(FusedArgs P, hipStream_t st);
 bool i8_w32_fits(const FusedArgs& P);
 template <bool Signed>
 int launch_i8_w32(FusedArgs P, hipStream_t st);
-bool i8_wide_lc_fits(const FusedArgs& P);
-template <bool Signed>
-int launch_i8_wide_lc(FusedArgs P, hipStream_t st);
 
 // Wide kernel (bf_wide.hip): returns BF_ERR_ARG without launching when the shape does not fit it.
 bool wide_fits(const FusedArgs& P);

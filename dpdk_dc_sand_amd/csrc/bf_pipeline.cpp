@@ -13,6 +13,7 @@
 // stream, so a frame submitted before an update uses the old model and every later frame the new one (stream
 // order), with no host synchronisation on the data path (an update waits only when kStage earlier updates are
 // still queued behind in-flight frames).
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -103,9 +104,11 @@ int bf_pipeline_create(bf_pipeline** out, int B, int C, int T, int A, int M, int
   BF_REQUIRE(delay_channels == 1 || delay_channels == C, "bf_pipeline_create: delay_channels must be 1 or C");
   BF_REQUIRE(depth >= 1 && depth <= 64, "bf_pipeline_create: depth=%d out of [1, 64]", depth);
   BF_REQUIRE(sample_period > 0.0, "bf_pipeline_create: sample_period must be > 0");
-  BF_REQUIRE((flags & ~(BF_FUSED_SIGNED | BF_FUSED_OUT_INT8 | BF_FUSED_EXACT_COEFF | BF_FUSED_INT8_VIA_F32 |
-                         BF_FUSED_PATH_MASK | BF_FUSED_ORDER_MASK)) == 0,
-             "bf_pipeline_create: unknown flags 0x%x", flags);
+  const char* ferr = bf::fused_flags_error(flags);
+  BF_REQUIRE(ferr == nullptr, "bf_pipeline_create: %s (flags 0x%x)", ferr, flags);
+  const bool q14 = (flags & BF_FUSED_OUT_INT8) && !(flags & BF_FUSED_INT8_VIA_F32);
+  BF_REQUIRE(!q14 || bf::q14_sum_bound_ok(A, flags & BF_FUSED_SIGNED, 1.0),
+             "bf_pipeline_create: n_ants=%d overflows the int8 path's int32 beam sums", A);
   auto* p = new bf_pipeline();
   p->B = B, p->C = C, p->T = T, p->A = A, p->M = M, p->Ctot = Ctot, p->xeng_id = xeng_id, p->flags = flags;
   p->delay_channels = delay_channels, p->depth = depth, p->ts = sample_period, p->out_scale = out_scale;
@@ -193,6 +196,18 @@ int bf_pipeline_set_gains(bf_pipeline* p, const float* host_gains) {
     p->gains_set = false;
     bf::clear_error();
     return BF_OK;
+  }
+  if ((p->flags & BF_FUSED_OUT_INT8) && !(p->flags & BF_FUSED_INT8_VIA_F32)) {
+    // the Q14 integer path: the weights must keep the high limb int8 and the int32 sums from wrapping
+    double gmax = 0.0;
+    const size_t n = static_cast<size_t>(p->M) * p->A;
+    for (size_t i = 0; i < n; ++i) {
+      const double g = std::fabs(static_cast<double>(host_gains[i]));
+      BF_REQUIRE(std::isfinite(g), "bf_pipeline_set_gains: weight %zu is not finite", i);
+      gmax = g > gmax ? g : gmax;
+    }
+    BF_REQUIRE(bf::q14_sum_bound_ok(p->A, p->flags & BF_FUSED_SIGNED, gmax),
+               "bf_pipeline_set_gains: weight magnitude %g out of range for int8 beams with %d inputs", gmax, p->A);
   }
   const int st = upload(p, host_gains, p->h_gains, p->d_gains, p->gain_bytes, p->ev_gains, &p->n_gain_updates);
   if (st == BF_OK) p->gains_set = true;

@@ -1,6 +1,8 @@
 // Runtime helpers of the C ABI: device memory, pinned host memory, streams and events over HIP.
 // These stand in for katsdpsigproc.accel's context/queue/DeviceArray (beamform_op_sequence_test.py:105-163)
 // and the CUDA-runtime calls of the C++ harness (common/UnitTest.cpp:28-111).
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 
 #include "bf_common.hpp"
@@ -20,13 +22,47 @@ void set_error(const char* fmt, ...) {
 
 void clear_error() { g_last_error.clear(); }
 
+// An empty kernel whose dispatches delimit a region in a profiler's kernel trace (bench.py: the timed steps).
+__global__ void bf_trace_mark_kernel(int tag) { (void)tag; }
+
+// splitmix64 of (seed, 16-byte chunk index): two words per lane, one 16-byte store.
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void bf_fill_random_kernel(uint8_t* dst, size_t bytes, unsigned long long seed) {
+  const size_t n16 = bytes / 16;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += static_cast<size_t>(gridDim.x) * 256) {
+    const unsigned long long a = splitmix64(seed ^ (2 * i)), b = splitmix64(seed ^ (2 * i + 1));
+    *reinterpret_cast<ulonglong2*>(dst + 16 * i) = ulonglong2{a, b};
+  }
+  const size_t tail = bytes - 16 * n16;  // the last < 16 bytes: one thread
+  if (blockIdx.x == 0 && threadIdx.x == 0 && tail) {
+    const unsigned long long a = splitmix64(seed ^ (2 * n16)), b = splitmix64(seed ^ (2 * n16 + 1));
+    for (size_t k = 0; k < tail; ++k) dst[16 * n16 + k] = static_cast<uint8_t>((k < 8 ? a >> (8 * k) : b >> (8 * (k - 8))));
+  }
+}
+
+int cu_count() {
+  static std::atomic<int> cache[64];  // per device index; 0 = not looked up yet
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev >= 0 && dev < 64 && (n = cache[dev].load(std::memory_order_relaxed)) > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  if (dev >= 0 && dev < 64) cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
 }  // namespace bf
 
 extern "C" {
 
 const char* bf_last_error(void) { return bf::g_last_error.c_str(); }
 
-int bf_abi_version(void) { return 100; }
+int bf_abi_version(void) { return 200; }
 
 int bf_device_count(int* count) {
   BF_REQUIRE(count != nullptr, "bf_device_count: null pointer");
@@ -159,6 +195,21 @@ int bf_event_record(void* event, void* stream) {
 int bf_event_synchronize(void* event) {
   BF_HIP(hipEventSynchronize(reinterpret_cast<hipEvent_t>(event)));
   return BF_OK;
+}
+
+int bf_fill_random(void* dst, size_t bytes, unsigned long long seed, void* stream) {
+  if (bytes == 0) return BF_OK;
+  BF_REQUIRE(dst != nullptr && (reinterpret_cast<uintptr_t>(dst) & 15) == 0, "bf_fill_random: null or misaligned");
+  const size_t chunks = (bytes + 15) / 16;
+  const unsigned grid = static_cast<unsigned>(std::min<size_t>((chunks + 255) / 256, 8192));
+  hipLaunchKernelGGL(bf::bf_fill_random_kernel, dim3(grid), dim3(256), 0, bf::as_stream(stream),
+                     static_cast<uint8_t*>(dst), bytes, seed);
+  BF_LAUNCHED("bf_fill_random_kernel");
+}
+
+int bf_trace_mark(int tag, void* stream) {
+  hipLaunchKernelGGL(bf::bf_trace_mark_kernel, dim3(1), dim3(64), 0, bf::as_stream(stream), tag);
+  BF_LAUNCHED("bf_trace_mark_kernel");
 }
 
 int bf_event_elapsed_ms(float* ms, void* start, void* stop) {

@@ -3,10 +3,19 @@
 The reference's only parallel axis is the X-engine index: engine `xeng_id` owns `n_channels_per_stream` channels
 whose absolute index is `c + n_channels_per_stream * xeng_id` (coeff_generator.py:49-53,
 coeff_generator_cpu.py:134-141).  Here rank r of a world of N is X-engine r.  Beamforming itself needs no collective;
-the only data movement is the optional root -> ranks channel scatter of a full-band voltage cube, done
-with `torch.distributed` (gloo on CPU, nccl = RCCL over xGMI on GPUs) and kept out of the timed hot path.
+the only data movement is the root -> ranks channel scatter of a full-band voltage cube, kept out of
+the timed hot path:
+  * `ChannelScatter`: device to device over RCCL/xGMI through libbf (bf_comm_create + bf_channel_scatter,
+    include/bf.h) -- the multi-GPU path;
+  * `scatter_channel_slices` / `gather_channel_slices`: host memory over a `rendezvous.HostGroup` -- rehearsals with
+    several ranks on one GPU (RCCL refuses two ranks on one device) and verification.
+No torch: every rank runs libbf on one HIP runtime.
 """
+import ctypes
+
 import numpy as np
+
+from . import _lib
 
 
 def shard_channels(n_channels, world_size):
@@ -21,40 +30,71 @@ def shard_channels(n_channels, world_size):
 def pack_channel_slices(raw, world_size):
     """Split a full-band raw cube (B, A, Ctot, T, 2, 2) into per-rank contiguous (B, A, C, T, 2, 2) cubes.
     A channel slice of the raw layout is B*A strided runs of C*T*4 bytes; packing makes each rank's part one
-    contiguous message."""
+    contiguous message (bf_channel_scatter does the same on the device with one 2-D copy per peer)."""
     raw = np.asarray(raw)
     Ctot = raw.shape[2]
     return [np.ascontiguousarray(raw[:, :, s:s + n]) for _, s, n in shard_channels(Ctot, world_size)]
 
 
-def scatter_channel_slices(raw, shape, dtype, rank, world_size, group=None, device=None):
-    """Root (rank 0) scatters the packed channel slices of `raw` (B, A, Ctot, T, 2, 2); every rank returns its
-    (B, A, Ctot / N, T, 2, 2) slice as a numpy array (CPU / gloo) or a torch tensor on `device` (nccl).
-
-    `shape` is the per-rank slice shape (all ranks must know it); `raw` is only read on rank 0."""
-    import torch
-    import torch.distributed as dist
-
-    tdtype = torch.from_numpy(np.zeros(1, dtype)).dtype
-    out = torch.empty(shape, dtype=tdtype, device=device)
-    if rank == 0:
-        parts = [torch.from_numpy(p).to(device) if device is not None else torch.from_numpy(p)
-                 for p in pack_channel_slices(raw, world_size)]
-        dist.scatter(out, scatter_list=parts, src=0, group=group)
-    else:
-        dist.scatter(out, src=0, group=group)
-    return out if device is not None else out.numpy()
+def scatter_channel_slices(raw, shape, dtype, group):
+    """Root (rank 0 of `group`, a rendezvous.HostGroup) scatters the packed channel slices of `raw`
+    (B, A, Ctot, T, 2, 2) through host memory; every rank returns its (B, A, Ctot / N, T, 2, 2) slice.  `shape` is
+    the per-rank slice shape (all ranks know it); `raw` is only read on rank 0."""
+    parts = [p.tobytes() for p in pack_channel_slices(raw, group.world)] if group.rank == 0 else None
+    mine = group.scatter_bytes(parts)
+    return np.frombuffer(mine, np.dtype(dtype)).reshape(shape).copy()
 
 
-def gather_channel_slices(part, rank, world_size, group=None):
-    """Inverse of scatter for beams (B, 2, C, T/16, 16, 2M) (verification only): rank 0 returns the full band."""
-    import torch
-    import torch.distributed as dist
+def gather_channel_slices(part, group):
+    """Inverse of the scatter for beams (B, 2, C, T/16, 16, 2M) (verification only): rank 0 returns the full band,
+    the other ranks None."""
+    part = np.ascontiguousarray(part)
+    got = group.gather_bytes(part.tobytes())
+    if got is None:
+        return None
+    return np.concatenate([np.frombuffer(g, part.dtype).reshape(part.shape) for g in got], axis=2)
 
-    t = torch.from_numpy(np.ascontiguousarray(part))
-    if rank == 0:
-        parts = [torch.empty_like(t) for _ in range(world_size)]
-        dist.gather(t, gather_list=parts, dst=0, group=group)
-        return np.concatenate([p.numpy() for p in parts], axis=2)
-    dist.gather(t, dst=0, group=group)
-    return None
+
+class ChannelScatter:
+    """The RCCL channel scatter of libbf (bf_comm_* / bf_channel_scatter).  Rank 0 makes the communicator id and
+    `group` (a rendezvous.HostGroup) hands it to every rank; the communicator lives on `context`'s device."""
+
+    def __init__(self, group, context):
+        self.group, self.context = group, context
+        self.rank, self.world = group.rank, group.world
+        uid, err = None, None
+        if self.rank == 0:
+            buf = ctypes.create_string_buffer(128)
+            try:
+                _lib.call("bf_comm_unique_id", buf, 128)
+                uid = buf.raw
+            except _lib.BeamformerError as e:  # every rank must learn it, or the others wait for an id forever
+                uid, err = b"", e
+        uid = group.broadcast_bytes(uid)
+        if not uid:
+            raise err or RuntimeError("rank 0 could not create the RCCL communicator id")
+        context.activate()
+        h = ctypes.c_void_p()
+        _lib.call("bf_comm_create", ctypes.byref(h), uid, len(uid), self.world, self.rank)
+        self.handle = h.value
+
+    def scatter(self, band, out, B, A, C, T, queue, root=0):
+        """Stream-ordered on `queue`: band (B, A, C*N, T, 2, 2) device array on `root` (None elsewhere) -> `out`
+        (B, A, C, T, 2, 2) device array on every rank."""
+        _lib.call("bf_channel_scatter", self.handle, _lib.ptr(band), _lib.ptr(out), B, A, C, T, root, queue.handle)
+
+    def allreduce_max(self, value):
+        v = ctypes.c_double(float(value))
+        _lib.call("bf_comm_allreduce_max", self.handle, ctypes.byref(v))
+        return v.value
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.call("bf_comm_destroy", self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

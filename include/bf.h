@@ -28,6 +28,7 @@ extern "C" {
 #define BF_ERR_ARG (-1)     /* invalid shape / argument (reference: template ValueError, prebeamform_reorder.py:62-65) */
 #define BF_ERR_HIP (-2)     /* HIP runtime error (reference: GPU_ERRCHK, common/Utils.hpp:8, common/Utils.cpp:8-16) */
 #define BF_ERR_NODEV (-3)   /* no GPU visible */
+#define BF_ERR_COMM (-4)    /* RCCL unavailable or a collective failed (multi-GPU channel scatter) */
 
 /* Thread-local message of the last failing call on this thread (replaces GPU_ERRCHK's stderr print). */
 const char* bf_last_error(void);
@@ -61,6 +62,9 @@ int bf_event_destroy(void* event);
 int bf_event_record(void* event, void* stream);
 int bf_event_synchronize(void* event);
 int bf_event_elapsed_ms(float* ms, void* start, void* stop);
+/* Launch one empty kernel (`bf_trace_mark_kernel`) on `stream`: its dispatches delimit a region of a profiler's
+ * kernel trace (bench.py brackets its timed steps with two of them; tools/kernel_stats.py reads the region). */
+int bf_trace_mark(int tag, void* stream);
 
 /* ---- hot path ----------------------------------------------------------------------------------------- */
 
@@ -123,11 +127,10 @@ int bf_beamform(const uint8_t* x, const float* w, float* y, int B, int P, int C,
 #define BF_FUSED_INT8_VIA_F32 8
 #define BF_FUSED_PATH_MASK 0x0f00
 #define BF_FUSED_PATH_ITEM 0x0100    /* one workgroup per (batch, channel) item (A <= 64, T <= 256), else generic */
-#define BF_FUSED_PATH_PIPE 0x0200    /* persistent double-buffered item kernel (float beams) */
 #define BF_FUSED_PATH_GENERIC 0x0300 /* any A, any T: groups of 64 antennas */
 #define BF_FUSED_PATH_WIDE 0x0400    /* many antennas x beams: multi-wave beam slabs (config 4) */
 #define BF_FUSED_PATH_WIDE16 0x0500  /* 16-beam slabs (float and int8 wide kernels) */
-#define BF_FUSED_PATH_STAGED 0x0600  /* int8 beams: loader/consumer waves of a persistent workgroup (A <= 256, M <= 64) */
+/* (0x0200 and 0x0600 named two measured-slower kernels of ABI 1.x, since removed: both are rejected as unknown.) */
 #define BF_FUSED_ORDER_MASK 0x3000
 #define BF_FUSED_ORDER_CHANNEL 0x1000 /* plain channel-fastest workgroup order */
 #define BF_FUSED_ORDER_XCD 0x2000     /* XCD-range order (XCD x streams channels [x C/8, (x+1) C/8)) */
@@ -173,6 +176,31 @@ int bf_pipeline_wait(bf_pipeline* p, long long ticket, int stage);         /* st
 int bf_pipeline_query(bf_pipeline* p, long long ticket, int stage, int* done);
 int bf_pipeline_flush(bf_pipeline* p);
 int bf_pipeline_stage_ms(bf_pipeline* p, long long ticket, float* h2d_ms, float* compute_ms, float* d2h_ms);
+
+/* ---- multi-GPU channel scatter --------------------------------------------------------------
+ * One process per GPU, rank r = X-engine r owning channels [C r, C (r+1)) of a C*N-channel band (the reference's
+ * absolute-channel convention, beamformer/beamforming/coeff_generator.py:49-53; its only multi-device pattern is a
+ * host thread per device, utilities/pcie_bandwidth_tests/main.cpp:193-224, which this replaces).  The hot path
+ * needs no collective; the root hands each rank its channel slice of a full-band cube once, device to device over
+ * RCCL/xGMI.  RCCL (/opt/rocm librccl.so.1) is loaded at the first bf_comm_* call.
+ *   bf_comm_unique_id : rank 0 makes the communicator id (BF_COMM_ID_BYTES); the caller hands it to every rank
+ *   bf_comm_create    : collective over all ranks, on the device current at the call
+ *   bf_channel_scatter: band (B, A, C*N, T, 2, 2) 8-bit on `root` (ignored elsewhere) -> slice (B, A, C, T, 2, 2) on
+ *                       every rank; stream-ordered on `stream` (root: per-peer 2-D pack + grouped ncclSend; peers:
+ *                       one ncclRecv); the root keeps a staging buffer of (N - 1) slices, grown on demand
+ *   bf_comm_allreduce_max: host value -> max over ranks (blocking; timing brackets and agreement checks) */
+#define BF_COMM_ID_BYTES 128
+typedef struct bf_comm bf_comm;
+int bf_comm_unique_id(void* id, size_t len);
+int bf_comm_create(bf_comm** out, const void* id, size_t len, int nranks, int rank);
+int bf_comm_destroy(bf_comm* comm);
+int bf_comm_allreduce_max(bf_comm* comm, double* value);
+int bf_channel_scatter(bf_comm* comm, const uint8_t* band, uint8_t* slice, int B, int A, int C, int T, int root,
+                       void* stream);
+
+/* Fill `bytes` of device memory with a deterministic pseudo-random byte stream (splitmix64 of seed and position):
+ * synthetic voltages made in HBM (bench.py's full-band cube at N GPUs), no host staging. */
+int bf_fill_random(void* dst, size_t bytes, unsigned long long seed, void* stream);
 
 /* Algorithmic HBM bytes of one bf_beamform_fused launch (bench / roofline bookkeeping). */
 double bf_fused_algorithmic_bytes(int B, int C, int T, int A, int M, int delay_channels, int out_int8);

@@ -42,7 +42,7 @@ def test_prototypes_match_header():
 
 def test_abi_version_and_error_channel():
     lib = _lib.load()
-    assert lib.bf_abi_version() == 100
+    assert lib.bf_abi_version() == 200
     assert isinstance(_lib.last_error(), str)
 
 
@@ -87,13 +87,21 @@ def test_pipeline_argument_validation_without_gpu():
     with pytest.raises(_lib.BeamformerError, match="null pipeline"):
         _lib.call("bf_pipeline_wait", None, 0, 1)
     assert _lib.load().bf_pipeline_destroy(None) == 0
+    # the fused call's flag checks, at creation (not at the first submit)
+    with pytest.raises(_lib.BeamformerError, match="unknown kernel path"):
+        _lib.call("bf_pipeline_create", ctypes.byref(h), 1, 4, 16, 4, 1, 64, 0, 1e-9, 0x700, 1.0, 1, 2)
+    with pytest.raises(_lib.BeamformerError, match="unknown workgroup order"):
+        _lib.call("bf_pipeline_create", ctypes.byref(h), 1, 4, 16, 4, 1, 64, 0, 1e-9, 0x3000, 1.0, 1, 2)
+    with pytest.raises(_lib.BeamformerError, match="overflows"):
+        _lib.call("bf_pipeline_create", ctypes.byref(h), 1, 4, 16, 364, 1, 64, 0, 1e-9, _lib.FUSED_OUT_INT8, 1.0, 1, 2)
 
 
 def test_kernel_path_and_contract_flags_are_validated():
     fake = 1 << 20
     args = [fake, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0]
-    with pytest.raises(_lib.BeamformerError, match="unknown kernel path"):
-        _lib.call("bf_beamform_fused", *args, 0x700, 1.0, None)
+    for retired in (0x200, 0x600, 0x700):  # 0x200 / 0x600: removed measured-slower kernels (ABI 1.x)
+        with pytest.raises(_lib.BeamformerError, match="unknown kernel path"):
+            _lib.call("bf_beamform_fused", *args, retired, 1.0, None)
     with pytest.raises(_lib.BeamformerError, match="unknown workgroup order"):
         _lib.call("bf_beamform_fused", *args, 0x3000, 1.0, None)
     # Q14 int8 contract: more uint8 antennas than the int32 beam sums hold (A * 255 * 23171 >= 2^31) is refused

@@ -1,13 +1,14 @@
 """Multi-rank channel sharding on the GPU through libbf, on the one visible MI355X.
 
-Two fresh child processes (ranks of a gloo world of 2) share the GPU.  Rank 0 holds a full-band raw cube; the
+Two fresh child processes (ranks of a TCP rendezvous group of 2, no torch) share the GPU.  Rank 0 holds a full-band raw cube; the
 channel scatter (dpdk_dc_sand_amd.shard) gives each rank its X-engine's contiguous channel slice; each rank beamforms
 its slice with `FusedBeamformerTemplate(..., xeng_id=rank)` -- the reference's absolute-channel convention
 `ichannel = c + C * xeng_id` (coeff_generator.py:49-53) -- and the beams are gathered back.  The gathered band must
 equal the full-band oracle: int8 bit-exact, float32 within the stated tolerance.
 
 `test_bench_multi_rank_rehearsal` runs bench.py itself under torch.distributed.run with two ranks on this GPU and
-the gloo scatter backend (RCCL cannot put two ranks on one device); the driver's 8-GPU run uses the nccl backend.
+the host scatter backend (RCCL cannot put two ranks on one device); the driver's 8-GPU run uses the RCCL backend
+(libbf bf_channel_scatter), whose one-rank form runs here.
 """
 import json
 import os
@@ -32,18 +33,15 @@ def _free_port():
 
 
 def _rank_main(rank, world, port, out_dir):
-    import torch.distributed as dist  # torch before libbf: one HIP runtime
-
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
     from dpdk_dc_sand_amd import accel
     from dpdk_dc_sand_amd.beamforming import FusedBeamformerTemplate
+    from dpdk_dc_sand_amd.rendezvous import HostGroup
     from dpdk_dc_sand_amd.shard import gather_channel_slices, scatter_channel_slices
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    group = HostGroup(rank, world, "127.0.0.1", port)
     try:
         B, A, M, T, C = 2, 64, 16, 256, 8
         Ctot = C * world
@@ -56,7 +54,7 @@ def _rank_main(rank, world, port, out_dir):
         d[..., 2] = rng.uniform(-np.pi, np.pi, (M, A))
         d[..., 3] = rng.uniform(-1, 1, (M, A))
         raw = rng.integers(-128, 128, (B, A, Ctot, T, 2, 2), dtype=np.int8) if rank == 0 else None
-        mine = scatter_channel_slices(raw, (B, A, C, T, 2, 2), np.int8, rank, world)
+        mine = scatter_channel_slices(raw, (B, A, C, T, 2, 2), np.int8, group)
 
         ctx = accel.create_some_context(device=0)
         queue = ctx.create_command_queue()
@@ -68,7 +66,7 @@ def _rank_main(rank, world, port, out_dir):
             op.buffer("inSamples").set(queue, mine)
             op.buffer("delay_vals").set(queue, d)
             op()
-            out[name] = gather_channel_slices(op.buffer("outData").get(queue), rank, world)
+            out[name] = gather_channel_slices(op.buffer("outData").get(queue), group)
         if rank == 0:
             q_ref = O.fused_beamform_int8(raw, d, Ctot, t0=1e-3, batch_dt=bdt, scale=1 / 64, signed=True)
             y_ref = O.fused_beamform(raw, d, Ctot, t0=1e-3, batch_dt=bdt, signed=True)
@@ -76,7 +74,7 @@ def _rank_main(rank, world, port, out_dir):
             np.savez(os.path.join(out_dir, "result.npz"), q=out["int8"], q_ref=q_ref, y=out["f32"], y_ref=y_ref,
                      x=O.reorder(raw), w=w)
     finally:
-        dist.destroy_process_group()
+        group.close()
 
 
 def test_channel_sharded_hip_beamforming_matches_full_band(tmp_path):
@@ -103,31 +101,34 @@ def test_channel_sharded_hip_beamforming_matches_full_band(tmp_path):
 
 def test_bench_multi_rank_rehearsal(tmp_path):
     """bench.py --gpus 2 under torch.distributed.run: both ranks time their own channel shard (X-engines 0 and 1),
-    the input arrives through the scatter (gloo backend here), and rank 0 prints one JSON line with the whole-job
-    value and the scatter report."""
+    the input arrives through the scatter (host backend here), and rank 0 prints one JSON line with the whole-job
+    value, the scatter report and the config-4 channel-sharded secondary lines."""
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
-           "--warmup", "1", "--settle-ms", "0", "--scatter-backend", "gloo", "--workload", "cfg2"]
+           "--warmup", "1", "--settle-ms", "0", "--scatter-backend", "host", "--workload", "cfg3", "--nbuf", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    assert line["scatter"]["backend"] == "gloo" and line["scatter"]["ranks"] == 2
+    assert line["scatter"]["backend"] == "host" and line["scatter"]["ranks"] == 2
     assert line["scatter"]["bytes_per_rank"] == 8 * 64 * 4096 * 256 * 4
     assert line["value"] > 0
+    sec = line["secondary"]
+    assert [s["workload"][:4] for s in sec] == ["cfg4", "cfg4"], sec
+    assert all("error" not in s and s["n_gpus"] == 2 and s["value"] > 0 for s in sec), sec
 
 
 def test_bench_rccl_scatter_path_one_rank(tmp_path):
-    """The RCCL side of the channel scatter on a one-GPU box: a one-rank "nccl" communicator runs bench.py's device
-    path end to end -- band generated in HBM, packed slices, torch.distributed scatter over RCCL, the received
-    device tensor bound as the operator's input and timed.  (More ranks than GPUs is not an RCCL configuration; the
-    N-rank run is the driver's multi-GPU node.)"""
+    """The RCCL side of the channel scatter on a one-GPU box: a one-rank libbf communicator runs bench.py's device
+    path end to end -- band filled in HBM, the id hand-out, bf_channel_scatter, the received slice bound as the
+    operator's input and timed.  (More ranks than GPUs is not an RCCL configuration; the N-rank run is the driver's
+    multi-GPU node.)"""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--settle-ms", "0",
-           "--scatter-backend", "nccl", "--scatter-at-one", "--workload", "cfg2", "--no-secondary", "--no-pmc",
-           "--no-cpu-baseline", "--no-ceiling"]
+           "--scatter-backend", "rccl", "--scatter-at-one", "--workload", "cfg2", "--no-secondary", "--no-pmc",
+           "--no-cpu-baseline", "--no-ceiling", "--no-rocprof"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -135,6 +136,35 @@ def test_bench_rccl_scatter_path_one_rank(tmp_path):
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
     sc = line["scatter"]
-    assert sc["backend"] == "nccl" and sc["ranks"] == 1 and "RCCL" in sc["collective"], sc
+    assert sc["backend"] == "rccl" and sc["ranks"] == 1 and "RCCL" in sc["collective"], sc
     assert sc["bytes_per_rank"] == 8 * 64 * 4096 * 256 * 4 and sc["seconds"] > 0
     assert line["value"] > 0
+
+
+def test_channel_scatter_one_rank_comm():
+    """libbf's communicator at one rank: the RCCL id, bf_comm_create, bf_comm_allreduce_max (an RCCL all-reduce) and
+    bf_channel_scatter of a (B, A, C, T, 2, 2) band into a slice (the root's own 2-D pack) equal the numpy slice; the
+    device RNG fill is deterministic."""
+    sys.path.insert(0, ROOT)
+    from dpdk_dc_sand_amd import _lib, accel
+    from dpdk_dc_sand_amd.rendezvous import HostGroup
+    from dpdk_dc_sand_amd.shard import ChannelScatter
+
+    ctx = accel.create_some_context(device=0)
+    q = ctx.create_command_queue()
+    comm = ChannelScatter(HostGroup(0, 1), ctx)
+    try:
+        assert comm.allreduce_max(3.25) == 3.25
+        B, A, C, T = 2, 3, 5, 32
+        band = accel.DeviceArray(ctx, (B, A, C, T, 2, 2), np.uint8)
+        _lib.call("bf_fill_random", band.ptr, band.nbytes, 7, q.handle)
+        host = band.get(q)
+        again = accel.DeviceArray(ctx, (B, A, C, T, 2, 2), np.uint8)
+        _lib.call("bf_fill_random", again.ptr, again.nbytes, 7, q.handle)
+        np.testing.assert_array_equal(again.get(q), host)
+        assert len(np.unique(host)) > 200
+        out = accel.DeviceArray(ctx, (B, A, C, T, 2, 2), np.uint8)
+        comm.scatter(band, out, B, A, C, T, q)
+        np.testing.assert_array_equal(out.get(q), host)
+    finally:
+        comm.close()

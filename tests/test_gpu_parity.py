@@ -241,6 +241,20 @@ def test_matrix_multiply_persistent_equals_ring(context, command_queue, T, signe
     assert_beams_allclose(y[:, :, sel], O.complex_mult(xs, ws, signed=signed), xs, ws, signed=signed)
 
 
+@pytest.mark.parametrize("B,C,M", [(1, 5, 16), (1, 7, 9), (3, 3, 12)])
+def test_matrix_multiply_persistent_single_slab_any_item_count(context, command_queue, B, C, M):
+    """256 antennas with 9..16 beams (one slab, no XCD item order) and a (b, p, c) item count that is not a multiple
+    of 8 (10, 14, 18 items): the persistent table kernel's grid needs no multiple of 8 there (such calls
+    were refused with BF_ERR_ARG)."""
+    A, T = 256, 64
+    rng = np.random.default_rng(B * 100 + C)
+    x = rng.integers(0, 256, (B, 2, C, T // 16, 16, A, 2), dtype=np.uint8)
+    w = rng.uniform(-1.0, 1.0, (B, 2, C, 2 * A, 2 * M)).astype(np.float32)
+    op = MatrixMultiplyTemplate(context, A, C, T, M, B).instantiate(command_queue)
+    (y,) = run(op, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
+    assert_beams_allclose(y, O.complex_mult(x, w), x, w)
+
+
 # ---- full sequence (beamform_op_sequence_test.py:37-200) ---------------------------------------------------
 def test_op_sequence_golden(context, command_queue):
     B, A, M, Ctot, T, C = (int(v) for v in get("opseq_cfg1", "dims"))
@@ -299,11 +313,10 @@ def test_fused_equals_op_sequence_bitwise(context, command_queue, fused_path):
                           O.coeffs(d, B, 2, C, Ctot, A, M, 2))
 
 
-@pytest.fixture(params=["auto", "item", "pipe", "generic", "wide", "wide16"])
+@pytest.fixture(params=["auto", "item", "generic", "wide", "wide16"])
 def fused_path(request):
     """Run a fused test through each kernel (FusedBeamformerTemplate kernel_path = BF_FUSED_PATH_* flags): the
-    automatic choice, the single-item kernel (A <= 64, T <= 256), the persistent pipelined kernel, the generic
-    kernel, and the wide kernel (many antennas x beams) with 32- and 16-beam slabs.  A path that does not fit a shape
+    automatic choice, the single-item kernel (A <= 64, T <= 256), the generic kernel, and the wide kernel (many antennas x beams) with 32- and 16-beam slabs.  A path that does not fit a shape
     falls through to one that does."""
     return request.param
 
@@ -337,7 +350,7 @@ def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C
     (4, 1, 16, 1024, 1, 16, True), (80, 24, 3, 16, 3, 1, True), (32, 8, 4, 64, 2, 1, False),
     (48, 12, 2, 128, 2, 1, False), (33, 5, 3, 80, 2, 3, True), (16, 8, 3, 48, 2, 1, True),
     (64, 16, 2, 112, 1, 1, False), (40, 32, 2, 64, 1, 2, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16", "staged"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16"])
 def test_fused_int8_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """int8 (requantised) beams: the integer MFMA path reproduces the oracle's integer contract bit for bit, on the
     item kernel (A <= 64, T <= 256; others fall through to generic) and the generic kernel (any A, T)."""
@@ -474,7 +487,7 @@ def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, 
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
     (64, 16, 3, 256, 2, 1, True), (64, 16, 2, 256, 2, 1, False), (19, 3, 4, 48, 2, 4, False),
     (130, 9, 2, 64, 1, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16", "staged"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16"])
 def test_fused_int8_beam_weights_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """Weighted int8 beams: Q14 limbs of the weighted float32 coefficients, bit-exact to the integer contract."""
     Ctot, xeng, t0, bdt = 4096, 2, 1e-3, 256 * 8192 * TS
@@ -513,7 +526,7 @@ def boundary_delays(M, A, seed):
 
 @pytest.mark.parametrize("A,M,C,T,B,signed", [(64, 16, 3, 256, 2, True), (64, 16, 2, 256, 2, False),
                                               (19, 3, 3, 48, 2, False), (256, 64, 1, 32, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16", "staged"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16"])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_fused_int8_rounding_boundaries(context, command_queue, i8_kernel, weighted, A, M, C, T, B,
                                         signed):

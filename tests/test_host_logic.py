@@ -136,14 +136,3 @@ def test_streaming_template():
     with pytest.raises(ValueError):
         StreamingBeamformerTemplate(None, 2, 8, 64, 32, 4, 3, depth=0)
 
-
-def test_loader_consumer_protocol_has_no_deadlock():
-    """The int8 loader/consumer wide kernel's LDS-counter hand-offs (bf_wide_i8lc.hip), modelled on the CPU and run
-    under random interleavings of 4 loaders and 1-4 consumers: every schedule completes."""
-    import importlib.util
-    spec = importlib.util.spec_from_file_location("lcsim", os.path.join(ROOT, "tools", "sim", "lc_protocol_sim.py"))
-    sim = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(sim)
-    for count, S, NQ, nact in [(16, 8, 4, 4), (3, 1, 1, 1), (7, 2, 1, 2), (9, 3, 2, 3), (2, 1, 1, 4)]:
-        for seed in range(3):
-            assert isinstance(sim.simulate(count, S, NQ, nact, seed=seed), int), (count, S, NQ, nact, seed)

@@ -1,19 +1,23 @@
-"""Multi-rank (X-engine) logic on CPU: world_size-2 gloo process groups.
+"""Multi-rank (X-engine) logic on CPU: world-2 and world-3 process groups over the TCP rendezvous.
 
-Checks the channel-shard arithmetic, the root -> ranks channel scatter / gather helpers, that beamforming each
-shard with xeng_id = rank reproduces the full-band result exactly (the reference's absolute-channel convention,
-coeff_generator.py:49-53), and bench.py's gloo timing bracket (barrier + max over ranks)."""
+Checks the channel-shard arithmetic, the host group's collectives (barrier, max, broadcast -- the RCCL id hand-out
+--, scatter, gather), the root -> ranks channel scatter / gather helpers, that beamforming each shard with
+xeng_id = rank reproduces the full-band result exactly (the reference's absolute-channel convention,
+coeff_generator.py:49-53), bench.py's timing bracket (barrier + max over ranks), and the C ABI's communicator
+argument checks (no GPU needed: they fail before RCCL is touched)."""
+import ctypes
+import multiprocessing as mp
 import os
 import socket
 import sys
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+from dpdk_dc_sand_amd import _lib  # noqa: E402
 from dpdk_dc_sand_amd.shard import pack_channel_slices, shard_channels  # noqa: E402
 
 
@@ -38,16 +42,53 @@ def test_pack_channel_slices_roundtrip():
     np.testing.assert_array_equal(np.concatenate(parts, axis=2), raw)
 
 
-def _worker(rank, world, port, result_q):
-    import torch.distributed as dist
+def _run_world(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return sorted(results)
 
-    import oracle as O
-    from dpdk_dc_sand_amd.shard import gather_channel_slices, scatter_channel_slices
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _group_worker(rank, world, port, q):
+    from dpdk_dc_sand_amd.rendezvous import HostGroup
     try:
+        g = HostGroup(rank, world, "127.0.0.1", port)
+        g.barrier()
+        mx = g.allreduce_max(10.0 - rank)
+        uid = g.broadcast_bytes(bytes(range(128)) if rank == 0 else None)  # the RCCL id hand-out
+        part = g.scatter_bytes([bytes([r]) * (r + 1) for r in range(world)] if rank == 0 else None)
+        got = g.gather_bytes(bytes([rank + 100]))
+        js = g.gather_json({"rank": rank})
+        anyf = g.allreduce_any(rank == world - 1)
+        g.barrier()
+        g.close()
+        q.put((rank, "ok", mx, uid == bytes(range(128)), part == bytes([rank]) * (rank + 1),
+               got == [bytes([r + 100]) for r in range(world)] if rank == 0 else got is None,
+               js == [{"rank": r} for r in range(world)] if rank == 0 else js is None, anyf))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, "error " + repr(e), None, None, None, None, None, None))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_group_collectives(world):
+    for rank, status, mx, uid_ok, part_ok, gather_ok, json_ok, anyf in _run_world(_group_worker, world):
+        assert status == "ok", status
+        assert mx == 10.0 and uid_ok and part_ok and gather_ok and json_ok and anyf, rank
+
+
+def _shard_worker(rank, world, port, q):
+    import oracle as O
+    from dpdk_dc_sand_amd.rendezvous import HostGroup
+    from dpdk_dc_sand_amd.shard import gather_channel_slices, scatter_channel_slices
+    try:
+        g = HostGroup(rank, world, "127.0.0.1", port)
         B, A, M, T, Ctot = 2, 5, 3, 32, 8
         C = Ctot // world
         raw = O.u8_voltages((B, A, Ctot, T, 2, 2), seed=11) if rank == 0 else None
@@ -55,37 +96,44 @@ def _worker(rank, world, port, result_q):
         rng = np.random.default_rng(3)
         d[..., 0] = rng.uniform(0, 10 * O.TS_MEERKAT, (1, M, A))
         d[..., 2] = rng.uniform(-np.pi, np.pi, (1, M, A))
-        mine = scatter_channel_slices(raw, (B, A, C, T, 2, 2), np.uint8, rank, world)
+        mine = scatter_channel_slices(raw, (B, A, C, T, 2, 2), np.uint8, g)
         beams = O.fused_beamform(mine, d, Ctot, xeng_id=rank)  # this X-engine's channels
-        full = gather_channel_slices(beams, rank, world)
+        full = gather_channel_slices(beams, g)
 
-        # bench.py's timing bracket: barrier + max over ranks
+        # bench.py's timing bracket: barrier + max over ranks, on the same kind of group
         from bench import Dist
-        os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank))
         dd = Dist.__new__(Dist)
-        dd.world, dd.rank, dd.local_rank, dd.dist = world, rank, rank, dist
+        dd.world, dd.rank, dd.local_rank, dd.group, dd.comm = world, rank, rank, g, None
         dd.barrier()
         mx = dd.max(float(rank + 1))
+        equal = None
         if rank == 0:
-            ref = O.fused_beamform(raw, d, Ctot, xeng_id=0)
-            result_q.put(("ok", bool(np.array_equal(full, ref)), mx))
+            equal = bool(np.array_equal(full, O.fused_beamform(raw, d, Ctot, xeng_id=0)))
+        g.close()
+        q.put((rank, "ok", equal, mx))
     except Exception as e:  # pragma: no cover - reported to the parent
-        result_q.put(("error", repr(e), None))
-    finally:
-        dist.destroy_process_group()
+        q.put((rank, "error " + repr(e), None, None))
 
 
-def test_channel_sharded_beamforming_matches_full_band_gloo():
+def test_channel_sharded_beamforming_matches_full_band():
     world = 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    status, equal, mx = q.get(timeout=240)
-    for p in procs:
-        p.join(timeout=60)
-    assert status == "ok", equal
-    assert equal, "sharded beams differ from the full-band result"
-    assert mx == float(world)
+    res = _run_world(_shard_worker, world)
+    assert all(r[1] == "ok" for r in res), res
+    assert res[0][2], "sharded beams differ from the full-band result"
+    assert all(r[3] == float(world) for r in res)
+
+
+def test_comm_argument_validation_without_gpu():
+    h = ctypes.c_void_p()
+    uid = bytes(128)
+    with pytest.raises(_lib.BeamformerError, match="null pointer"):
+        _lib.call("bf_comm_create", None, uid, 128, 2, 0)
+    with pytest.raises(_lib.BeamformerError, match="128 bytes"):
+        _lib.call("bf_comm_create", ctypes.byref(h), uid, 64, 2, 0)
+    with pytest.raises(_lib.BeamformerError, match="rank 2 of 2"):
+        _lib.call("bf_comm_create", ctypes.byref(h), uid, 128, 2, 2)
+    with pytest.raises(_lib.BeamformerError, match="128-byte buffer"):
+        _lib.call("bf_comm_unique_id", ctypes.create_string_buffer(16), 16)
+    with pytest.raises(_lib.BeamformerError, match="null pointer"):
+        _lib.call("bf_channel_scatter", None, None, None, 1, 1, 1, 16, 0, None)
+    assert _lib.load().bf_comm_destroy(None) == 0

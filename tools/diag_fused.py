@@ -87,7 +87,7 @@ if "w8" in _os.environ.get("DIAG_KERNELS", ""):
     if _os.environ.get("W8_MODES"):
         w8names = {int(m): w8names.get(int(m), str(m)) for m in _os.environ["W8_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
-    alg8 = nin + nout // 4 // 4  # int8 beams: 2 B per complex beam sample vs 8
+    alg8 = nin + nout // 4  # int8 beams: 2 B per complex beam sample vs 8 (r2's files used nout // 16: understated)
     res = {m: [] for m in w8names}
     for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
         for mode in w8names:
@@ -107,32 +107,6 @@ if "w8" in _os.environ.get("DIAG_KERNELS", ""):
         ts = sorted(res[mode])
         print(f"  w8 mode {mode:2d} {w8names[mode]:18s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
               f"alg {alg8 / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
-if "lc" in _os.environ.get("DIAG_KERNELS", ""):
-    lib.bf_diag_lc.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
-    lcnames = {0: "full", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store", 8: "no-load",
-               9: "no-coef,no-load", 11: "no-coef,no-mfma,no-load", 15: "barriers+lds only"}
-    if _os.environ.get("LC_MODES"):
-        lcnames = {int(m): lcnames.get(int(m), str(m)) for m in _os.environ["LC_MODES"].split(",")}
-    Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
-    alg8 = nin + nout // 4 // 4
-    res = {m: [] for m in lcnames}
-    for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
-        for mode in lcnames:
-            res[mode].append(timeit(lambda i: lib.bf_diag_lc(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
-                                                             B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
-    for mode in lcnames:
-        ts = sorted(res[mode])
-        print(f"  lc mode {mode:2d} {lcnames[mode]:26s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
-              f"alg {alg8 / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
-    for smode in (16, 17):  # phase stamps (s_memtime cycles per wave, averaged over workgroups)
-        q.finish()
-        assert lib.bf_diag_lc(smode, bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, B, C, T, A, M, Ctot, 1 / 1712e6, q.handle) == 0
-        q.finish()
-        raw = bufs[0][1].get(q)[: 256 * 8 * 8 * 8].view(np.uint64).reshape(256, 8, 8).astype(np.float64)
-        cons, lod = raw[:, :4, :5].mean(axis=(0, 1)), raw[:, 4:, :4].mean(axis=(0, 1))
-        print(f"  lc stamps mode {smode}: consumer total {cons[0]:.0f} cyc: table-wait {cons[1]:.0f} slot-wait "
-              f"{cons[2]:.0f} steps {cons[3]:.0f} stores {cons[4]:.0f} | loader total {lod[0]:.0f}: table {lod[1]:.0f} "
-              f"slot-wait {lod[2]:.0f} ring {lod[3]:.0f}")
 names_i8 = {0: "full (fast+fixup coef, occ 3)", 128: "exact-only coef", 16: "fast coef (inexact)", 1: "no-coef", 2: "no-mfma", 3: "no-coef,no-mfma", 4: "no-store",
             5: "no-coef,no-store", 7: "loads only", 8: "no-load", 64: "occupancy 2", 32: "contig stores(bad)",
             65: "occ 2, no-store", 1024: "serial coef", 2048: "pol order", 3072: "serial+pol order",
@@ -149,11 +123,11 @@ if _os.environ.get("I8_AB"):  # interleaved A/B: int8 item kernel with uniform-b
     for form, ts in ab.items():
         ts = sorted(ts)
         print(f"  i8 full, {form:8s} addressing  median {ts[len(ts) // 2] * 1e6:8.1f} us  min {ts[0] * 1e6:8.1f} us")
-for kbase, kname in ((0, "pipe"), (32, "item"), (512, "i8")):
-    if _os.environ.get("DIAG_KERNELS", "item,pipe,i8").find(kname) < 0:
+for kbase, kname in ((32, "item"), (512, "i8")):
+    if _os.environ.get("DIAG_KERNELS", "item,i8").find(kname) < 0:
         continue
     only = _os.environ.get("DIAG_MODES")
-    modes = [m for m in (names_i8 if kname == "i8" else names) if not (kname == "pipe" and m >= 64)]
+    modes = list(names_i8 if kname == "i8" else names)
     if only:
         modes = [m for m in modes if str(m) in only.split(",")]
     res = {m: [] for m in modes}
