@@ -6,7 +6,7 @@ CSRC     := dpdk_dc_sand_amd/csrc
 LIB      := dpdk_dc_sand_amd/libbf.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -munsafe-fp-atomics
 SRCS     := $(CSRC)/bf_runtime.cpp $(CSRC)/bf_coeff.hip $(CSRC)/bf_reorder.hip $(CSRC)/bf_beamform.hip \
-            $(CSRC)/bf_fused.hip $(CSRC)/bf_wide.hip $(CSRC)/bf_wide_i8.hip $(CSRC)/bf_requant.hip \
+            $(CSRC)/bf_fused.hip $(CSRC)/bf_wide.hip $(CSRC)/bf_wide_i8.hip $(CSRC)/bf_q14table.hip $(CSRC)/bf_requant.hip \
             $(CSRC)/bf_pipeline.cpp $(CSRC)/bf_comm.cpp
 OBJS     := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 HDRS     := $(wildcard $(CSRC)/*.hpp) include/bf.h
@@ -42,7 +42,10 @@ clean:
 
 # Diagnostic build (ablation variants + HBM stream kernel); used only by tools/diag_*.py, never by the product.
 DIAG_LIB := build/libbf_diag.so
+DIAG_OBJS := $(patsubst $(CSRC)/%,build/diag/%.o,$(SRCS))
 diag: $(DIAG_LIB)
-$(DIAG_LIB): $(SRCS) $(HDRS)
-	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -DBF_DIAG -shared -o $@ $(SRCS) -ldl
+build/diag/%.o: $(CSRC)/% $(HDRS)
+	@mkdir -p build/diag
+	$(HIPCC) $(HIPFLAGS) -DBF_DIAG -x hip -c $< -o $@
+$(DIAG_LIB): $(DIAG_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(DIAG_OBJS) -ldl
