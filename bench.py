@@ -80,6 +80,8 @@ def parse():
     p.add_argument("--scatter-at-one", action="store_true",
                    help="run the scatter path at N = 1 as well (a one-rank RCCL communicator: exercises the device "
                         "band, the libbf scatter and the binding of the received slice on a one-GPU box)")
+    p.add_argument("--coeff-table", choices=("on", "off"), default="on",
+                   help="int8 wide path (config 4): Q14 coefficients from the generated table (on) or in-kernel")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-secondary", action="store_true")
@@ -202,7 +204,8 @@ def template(args, dist, wl, int8_contract=None, kernel_path="auto"):
     return FusedBeamformerTemplate(args.ctx, B, C, Ctot, T, A, M, xeng_id=dist.rank, sample_period=TS,
                                    delay_channels=1, sample_signed=not args.unsigned, out_int8=args.out_int8,
                                    out_scale=1 / 64, t0=0.0, batch_dt=T * 2 * Ctot * TS,
-                                   int8_contract=int8_contract or args.int8_contract, kernel_path=kernel_path)
+                                   int8_contract=int8_contract or args.int8_contract, kernel_path=kernel_path,
+                                   coeff_table=args.coeff_table == "on")
 
 
 def delay_model(np, rng, shape):
@@ -443,7 +446,8 @@ def rocprof_check(args, n_secondary):
     cmd = [exe, "--kernel-trace", "--output-format", "csv", "-d", out, "-o", "bench", "--", sys.executable,
            os.path.abspath(__file__), "--prof-child", "--workload", args.workload, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--settle-ms", str(args.settle_ms), "--output", args.output,
-           "--int8-contract", args.int8_contract, "--no-pmc", "--no-cpu-baseline", "--no-ceiling"]
+           "--int8-contract", args.int8_contract, "--coeff-table", args.coeff_table, "--no-pmc", "--no-cpu-baseline",
+           "--no-ceiling"]
     cmd += (["--unsigned"] if args.unsigned else []) + (["--no-secondary"] if n_secondary == 0 else [])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
     files = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
@@ -468,9 +472,17 @@ def rocprof_entry(regions, i, kernel, alg_bytes):
     name, s = kernel_stats.dominant(regions[i], "::" + kernel + "<")
     if s is None:
         return {"error": f"no {kernel} dispatches in timed region {i}"}
-    return {"kernel_instance": name, "timed_dispatches": s["Calls"], "avg_us": round(s["AverageNs"] / 1e3, 2),
-            "median_us": round(s["MedianNs"] / 1e3, 2), "max_us": round(s["MaxNs"] / 1e3, 2),
-            "frac": round(alg_bytes / (s["AverageNs"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)}
+    steps = s["Calls"]
+    # every kernel of the timed steps (config 4's int8 path: the coefficient generator + the contraction)
+    per_step_ns = sum(v["TotalDurationNs"] for v in regions[i].values()) / steps
+    out = {"kernel_instance": name, "timed_dispatches": steps, "avg_us": round(s["AverageNs"] / 1e3, 2),
+           "median_us": round(s["MedianNs"] / 1e3, 2), "max_us": round(s["MaxNs"] / 1e3, 2),
+           "frac": round(alg_bytes / (per_step_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)}
+    if len(regions[i]) > 1:
+        out["per_step_us_all_kernels"] = round(per_step_ns / 1e3, 2)
+        out["kernels_us_per_step"] = {k.split("(")[0].split("::")[-1][:60]: round(v["TotalDurationNs"] / steps / 1e3, 2)
+                                      for k, v in regions[i].items()}
+    return out
 
 
 def compute_desc(out_int8, int8_contract):

@@ -57,6 +57,12 @@ PROTOTYPES = {
     "bf_beamform_fused_weighted": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                            c_int, c_int, c_int, c_double, c_double, c_double, c_int, c_float,
                                            c_void_p]),
+    "bf_fused_workspace_bytes": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P_size_t]),
+    "bf_beamform_fused_ws": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                     c_int, c_int, c_int, c_double, c_double, c_double, c_int, c_float, c_void_p,
+                                     c_size_t, c_void_p]),
+    "bf_q14_coeffs": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                              c_double, c_double, c_double, c_void_p]),
     "bf_pipeline_create": (c_int, [P_void, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_int,
                                    c_float, c_int, c_int]),
     "bf_pipeline_destroy": (c_int, [c_void_p]),

@@ -17,6 +17,8 @@ Per-block regeneration (BeamformerParameters.h:17 ACCUMULATIONS_BEFORE_NEW_COEFF
 time-dependent kernels BeamformerKernels.cu:121-189 and the fused study kernel :192-367): batch b is steered
 at dt_b = t0 + b * batch_dt using the delay and phase rates (SURVEY A3 convention).
 """
+import ctypes
+
 import numpy as np
 
 from .. import _lib, accel
@@ -41,6 +43,10 @@ class FusedBeamformerTemplate:
         integer MFMA path) or "f32" (requantised float32 beams: the reference's float32 coefficient arithmetic).
     kernel_path, workgroup_order: force a kernel path ("auto", "item", "generic", "wide", "wide16") or
         workgroup order ("auto", "channel", "xcd") -- tests and measurement; every path computes the same contract.
+    coeff_table: let the int8 wide path (many antennas x beams, e.g. config 4) take its Q14 coefficients from a
+        table generated just before each launch by the wavefront-parallel phasor kernel (bf_beamform_fused_ws: a
+        device workspace of `workspace_bytes` the operator allocates once) rather than evaluating every phasor in
+        the contraction kernel.  Same contract, same bits; default True.  Other shapes/paths need no workspace.
     """
 
     # int32 bound of the Q14 contract: |Wc| + |Ws| <= sqrt(2) * 2^14 * |g| + 1 per coefficient
@@ -53,7 +59,7 @@ class FusedBeamformerTemplate:
                  sample_period: float = 1 / 1712e6, delay_channels=None, sample_signed: bool = False,
                  out_int8: bool = False, out_scale: float = 1.0, t0: float = 0.0, batch_dt: float = 0.0,
                  exact_coeffs: bool = False, beam_weights: bool = False, int8_contract: str = "q14",
-                 kernel_path: str = "auto", workgroup_order: str = "auto") -> None:
+                 kernel_path: str = "auto", workgroup_order: str = "auto", coeff_table: bool = True) -> None:
         for name, v in dict(n_batches=n_batches, n_channels_per_stream=n_channels_per_stream, n_channels=n_channels,
                             n_samples_per_channel=n_samples_per_channel, n_ants=n_ants, n_beams=n_beams).items():
             if int(v) <= 0:
@@ -107,6 +113,12 @@ class FusedBeamformerTemplate:
         self.delay_shape = (delay_channels, M, A, 4)
         self.output_shape = (B, 2, C, T // 16, 16, 2 * M)
         self.weights_shape = (M, A)
+        self.coeff_table = bool(coeff_table)
+        self.workspace_bytes = 0
+        if self.coeff_table:
+            n = ctypes.c_size_t(0)
+            _lib.call("bf_fused_workspace_bytes", B, C, T, A, M, self.flags, ctypes.byref(n))
+            self.workspace_bytes = int(n.value)
 
     def check_weights(self, weights):
         """Validate an (M, A) weight table for this configuration; returns it as float32.  The int8 output's
@@ -148,6 +160,7 @@ class FusedBeamformer(accel.Operation):
         self.slots["delay_vals"] = accel.IOSlot(t.delay_shape, np.float32)
         self.slots["outData"] = accel.IOSlot(t.output_shape, np.int8 if t.out_int8 else np.float32)
         self._weights = None
+        self._workspace = None  # the Q14 coefficient table of the int8 wide path (allocated on first use)
         if t.beam_weights:
             self.slots["beamWeights"] = accel.IOSlot(t.weights_shape, np.float32)
             self._weights = np.ones(t.weights_shape, np.float32)
@@ -184,7 +197,10 @@ class FusedBeamformer(accel.Operation):
                 buf.set_async(self.command_queue, self._weights)
                 self._weights_dirty = False
             gains = buf.ptr
-        _lib.call("bf_beamform_fused_weighted", self.buffer("inSamples").ptr, self.buffer("delay_vals").ptr,
+        if t.workspace_bytes and self._workspace is None:
+            self._workspace = accel.DeviceArray(self.command_queue.context, (t.workspace_bytes,), np.uint8)
+        ws = self._workspace.ptr if self._workspace is not None else None
+        _lib.call("bf_beamform_fused_ws", self.buffer("inSamples").ptr, self.buffer("delay_vals").ptr,
                   t.delay_channels, gains, self.buffer("outData").ptr, t.n_batches, t.n_channels_per_stream,
                   t.n_samples_per_channel, t.n_ants, t.n_beams, t.n_channels, t.xeng_id, float(t.sample_period),
-                  t.t0, t.batch_dt, t.flags, t.out_scale, self.command_queue.handle)
+                  t.t0, t.batch_dt, t.flags, t.out_scale, ws, t.workspace_bytes, self.command_queue.handle)

@@ -1215,6 +1215,33 @@ extern "C" int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay
                                           const float* gains, void* y, int B, int C, int T, int A, int M, int Ctot,
                                           int xeng_id, double sample_period, double t0, double batch_dt, int flags,
                                           float out_scale, void* stream) {
+  return bf_beamform_fused_ws(raw, delay_vals, delay_channels, gains, y, B, C, T, A, M, Ctot, xeng_id, sample_period,
+                              t0, batch_dt, flags, out_scale, nullptr, 0, stream);
+}
+
+// The workspace the automatic path of bf_beamform_fused_ws can use: the int8 wide path's Q14 coefficient table
+// (bf_q14table.hip) when the shape takes the 32-beam int8 kernel, else 0.
+extern "C" int bf_fused_workspace_bytes(int B, int C, int T, int A, int M, int flags, size_t* bytes) {
+  BF_REQUIRE(bytes != nullptr, "bf_fused_workspace_bytes: null pointer");
+  *bytes = 0;
+  BF_REQUIRE(B > 0 && C > 0 && T > 0 && A > 0 && M > 0, "bf_fused_workspace_bytes: bad shape");
+  const char* ferr = bf::fused_flags_error(flags);
+  BF_REQUIRE(ferr == nullptr, "bf_fused_workspace_bytes: %s (flags 0x%x)", ferr, flags);
+  const int path = flags & BF_FUSED_PATH_MASK;
+  if ((flags & BF_FUSED_OUT_INT8) && !(flags & BF_FUSED_INT8_VIA_F32) && (path == 0 || path == BF_FUSED_PATH_WIDE)) {
+    bf::FusedArgs P{};
+    P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
+    const bool small = (2 * A + 63) / 64 <= 2 && T <= 256;
+    if ((path == BF_FUSED_PATH_WIDE || !small) && bf::i8_w32_fits(P) && bf::w32_table_fits(A))
+      *bytes = bf::w32_table_bytes(B, C, A, M);
+  }
+  return BF_OK;
+}
+
+extern "C" int bf_beamform_fused_ws(const uint8_t* raw, const float* delay_vals, int delay_channels,
+                                    const float* gains, void* y, int B, int C, int T, int A, int M, int Ctot,
+                                    int xeng_id, double sample_period, double t0, double batch_dt, int flags,
+                                    float out_scale, void* workspace, size_t workspace_bytes, void* stream) {
   BF_REQUIRE(raw && delay_vals && y, "bf_beamform_fused: null pointer");
   BF_REQUIRE(B > 0 && C > 0 && T > 0 && A > 0 && M > 0 && Ctot > 0 && xeng_id >= 0,
              "bf_beamform_fused: bad shape B=%d C=%d T=%d A=%d M=%d Ctot=%d", B, C, T, A, M, Ctot);
@@ -1231,6 +1258,9 @@ extern "C" int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay
   P.dv = reinterpret_cast<const float4*>(delay_vals);
   P.gain = gains;
   P.y = y;
+  BF_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "bf_beamform_fused: misaligned workspace");
+  P.table = static_cast<const uint32_t*>(workspace);
+  P.table_bytes = workspace ? workspace_bytes : 0;
   P.delay_channels = delay_channels;
   P.B = B;
   P.C = C;

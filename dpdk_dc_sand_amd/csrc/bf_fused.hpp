@@ -14,6 +14,8 @@ struct FusedArgs {
   const uint8_t* raw;
   const float4* dv;
   const float* gain;  // optional (M, A) real per-input beam weights (?beam-weights), folded into the phasors
+  const uint32_t* table;  // optional workspace for the int8 wide path's Q14 table (kLayoutW32, bf_q14table.hip)
+  size_t table_bytes;
   void* y;
   int delay_channels, B, C, T, A, M, S, NT, nslabs, xcd_order;
   int path, order;  // BF_FUSED_PATH_* and BF_FUSED_ORDER_* bits of the launch flags (0 = automatic)
@@ -88,6 +90,18 @@ __device__ __forceinline__ void lds_barrier() {
 
 // Kernel-path override of a launch (flags & BF_FUSED_PATH_MASK): 0 automatic, else one of the BF_FUSED_PATH_* values.
 inline int fused_kernel_choice(const FusedArgs& P) { return P.path; }
+
+// Q14 coefficient tables (bf_q14table.hip): (B, C, M, A) words, or the 32-beam int8 kernel's item layout.
+constexpr int kLayoutNatural = 0, kLayoutW32 = 1;
+// k-steps of 32 antennas of the 32-beam int8 kernel, padded to a multiple of 4 (its four-buffer rotation)
+__host__ __device__ inline int w32_table_steps(int A) { return 4 * ((((A + 31) >> 5) + 3) / 4); }
+// The table-driven 32-beam kernel stages at most 4 units of 8 words per thread: Sp <= 8 (A <= 256).
+__host__ __device__ inline bool w32_table_fits(int A) { return w32_table_steps(A) <= 8; }
+// Bytes of the kLayoutW32 table of one launch: 1024 Sp words per (b, c, 32-beam slab).
+inline size_t w32_table_bytes(int B, int C, int A, int M) {
+  return static_cast<size_t>(B) * C * ((M + 31) / 32) * 1024 * w32_table_steps(A) * 4;
+}
+int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t st);
 
 // Integer wide kernels: int8 beams for many antennas x beams.  bf_wide_i8.hip: a workgroup per 32-beam slab (the
 // default, BF_FUSED_PATH_WIDE) or per 16-beam slab (BF_FUSED_PATH_WIDE16).

@@ -32,6 +32,8 @@ struct bf_pipeline {
   std::vector<hipEvent_t> ev;
   float* d_delays = nullptr;
   float* d_gains = nullptr;
+  void* d_workspace = nullptr;  // the fused call's workspace (int8 wide path's Q14 table), used on s_comp only
+  size_t workspace_bytes = 0;
   // pinned staging rings for control updates: update u uses stage u % kStage, whose previous upload must have
   // retired (its event) -- so only kStage updates in flight at once can make the caller wait
   float* h_delays[kStage] = {};
@@ -79,6 +81,7 @@ void release(bf_pipeline* p) {
   }
   if (p->d_delays) (void)hipFree(p->d_delays);
   if (p->d_gains) (void)hipFree(p->d_gains);
+  if (p->d_workspace) (void)hipFree(p->d_workspace);
   if (p->s_h2d) (void)hipStreamDestroy(p->s_h2d);
   if (p->s_comp) (void)hipStreamDestroy(p->s_comp);
   if (p->s_d2h) (void)hipStreamDestroy(p->s_d2h);
@@ -147,6 +150,9 @@ int bf_pipeline_create(bf_pipeline** out, int B, int C, int T, int A, int M, int
   }
   if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_delays), p->delay_bytes)) != hipSuccess) return fail(e, "malloc");
   if ((e = hipMalloc(reinterpret_cast<void**>(&p->d_gains), p->gain_bytes)) != hipSuccess) return fail(e, "malloc");
+  if (bf_fused_workspace_bytes(B, C, T, A, M, flags, &p->workspace_bytes) == BF_OK && p->workspace_bytes > 0 &&
+      (e = hipMalloc(&p->d_workspace, p->workspace_bytes)) != hipSuccess)
+    return fail(e, "hipMalloc(workspace)");
   *out = p;
   bf::clear_error();
   return BF_OK;
@@ -231,10 +237,10 @@ int bf_pipeline_submit(bf_pipeline* p, const void* host_in, void* host_out, doub
 
   BF_HIP(hipStreamWaitEvent(p->s_comp, slot_event(p, n, 1), 0));
   BF_HIP(hipEventRecord(slot_event(p, n, 2), p->s_comp));
-  const int st = bf_beamform_fused_weighted(static_cast<const uint8_t*>(p->d_in[slot]), p->d_delays,
-                                            p->delay_channels, p->gains_set ? p->d_gains : nullptr, p->d_out[slot],
-                                            p->B, p->C, p->T, p->A, p->M, p->Ctot, p->xeng_id, p->ts, t0, batch_dt,
-                                            p->flags, p->out_scale, p->s_comp);
+  const int st = bf_beamform_fused_ws(static_cast<const uint8_t*>(p->d_in[slot]), p->d_delays, p->delay_channels,
+                                      p->gains_set ? p->d_gains : nullptr, p->d_out[slot], p->B, p->C, p->T, p->A,
+                                      p->M, p->Ctot, p->xeng_id, p->ts, t0, batch_dt, p->flags, p->out_scale,
+                                      p->d_workspace, p->workspace_bytes, p->s_comp);
   if (st != BF_OK) return st;
   BF_HIP(hipEventRecord(slot_event(p, n, 3), p->s_comp));
 

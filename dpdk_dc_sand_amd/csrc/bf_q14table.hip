@@ -1,0 +1,177 @@
+// Q14 steering-coefficient generator of the integer (int8-beam) path: the wavefront-parallel phasor kernel.
+//
+// The reference generates its steering coefficients in a kernel of its own (beamformer/beamforming/
+// coeff_generator.py:12-103 writes a (B, P, C, 2A, 2M) float table; the C++ study's calculate_beamweights_*
+// kernels, beamformer_coefficient_generator/BeamformerKernels.cu:7-189, one sincos per coefficient).  Here the int8
+// path's coefficients -- W = rne(2^14 * RN32(g * RN32(cos rot))) and the same for sin (oracle quantise_coeffs of
+// fused_tables), rot = the reference's float64 phase -- are written compactly, one uint32 (Wc | Ws << 16) per
+// (b, c, m, a): 4 bytes where the reference writes 16 per coefficient and per (b, p).
+//
+// Cost.  With one delay model for every channel (delay_channels == 1) the phase is linear in the channel,
+// rot(ch) = phi' + tau' (ch - Ctot/2) K, so a thread owns one (a, m) and walks a run of kRun consecutive channels:
+// the phasor of the run's first channel from the float64 sincos (fdlibm kernels, <= 1 ulp), then one float64
+// complex multiply by e^{i tau' K} per channel (<= 64 roundings: < 1e-13 drift, re-anchored every run).  Each
+// component's Q14 value is decided on that float64 value +- kQ14Eps (bf_phase.hpp q14_pair: both sides give the
+// same Q14 value, so it is the contract's; the recurrence's error is four orders below the guard); a component
+// without a decision (~1e-5 of them), or a phase beyond the guard's validated range, is evaluated exactly
+// (q14_exact: the float64 phase in the reference's operation order).  ~30 VALU per coefficient against ~80 for a
+// fresh fast phasor.  Per-channel delay models (delay_channels == C) evaluate every channel with q14_fast.
+//
+// Layouts.  kLayoutNatural: (B, C, M, A) words (bf_q14_coeffs, include/bf.h).  kLayoutW32: the item layout the
+// table-driven 32-beam int8 kernel stages into LDS (bf_wide_i8.hip): per (b, c, 32-beam slab) 1024 Sp words, word
+// w = ((u >> 8) * 2 + (i >> 2)) * 1024 + (u & 255) * 4 + (i & 3) for unit u = (g << 5) | ml (beam ml of the slab,
+// slot-antenna group g of 8) and slot antenna i of the group -- one 16-byte load per lane per half unit there, and
+// 256 contiguous bytes per wave-store here.
+#include <algorithm>
+
+#include "bf_fused.hpp"
+
+namespace bf {
+
+namespace {
+
+constexpr int kQ14Run = 64;  // channels per thread (re-anchored per run)
+
+struct Q14TableArgs {
+  const float4* dv;
+  const float* gain;
+  uint32_t* out;
+  int delay_channels, B, C, A, M, Sp, nslabs, layout;
+  long long base_ch;
+  double ctot, ts, k, t0, batch_dt;
+};
+
+// Slot antenna sa of the w32 kernel's LDS image -> antenna (w8_step_base: the last step pulled back to [A - 32, A));
+// false for a row an earlier step already covers or a padded step.
+__device__ __forceinline__ bool w32_slot_antenna(int sa, int A, int* a) {
+  const int st = sa >> 5;
+  *a = min(32 * st, A - 32) + (sa & 31);
+  return *a >= 32 * st && *a < A;
+}
+
+template <bool Gain>
+__global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
+  const int b = blockIdx.z;
+  const int c0 = blockIdx.y * kQ14Run;
+  const int w = blockIdx.x * 256 + threadIdx.x;  // word within a (b, c[, slab]) block
+  int a, m, slab = 0;
+  bool valid;
+  size_t words, base;  // words per channel block; the block of (b, c0)
+  if (P.layout == kLayoutNatural) {
+    words = static_cast<size_t>(P.M) * P.A;
+    if (w >= static_cast<int>(words)) return;
+    m = w / P.A;
+    a = w - m * P.A;
+    valid = true;
+    base = (static_cast<size_t>(b) * P.C + c0) * words + w;
+  } else {
+    const int per_slab = 1024 * P.Sp;
+    slab = w / per_slab;
+    if (slab >= P.nslabs) return;
+    const int r = w - slab * per_slab;
+    const int u = ((r >> 11) << 8) | ((r >> 2) & 255), i = (((r >> 10) & 1) << 2) | (r & 3);
+    const int ml = u & 31, g = u >> 5;
+    m = slab * 32 + ml;
+    valid = w32_slot_antenna(8 * g + i, P.A, &a) && m < P.M;
+    words = static_cast<size_t>(per_slab) * P.nslabs;
+    base = (static_cast<size_t>(b) * P.C + c0) * words + w;
+  }
+  const int nrun = min(kQ14Run, P.C - c0);
+  uint32_t* o = P.out + base;
+  if (!valid) {
+    for (int j = 0; j < nrun; ++j) o[static_cast<size_t>(j) * words] = 0u;
+    return;
+  }
+  const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
+  const float g = Gain ? P.gain[static_cast<size_t>(m) * P.A + a] : 1.0f;
+  const float gq = g * 16384.0f;
+  const double half = P.ctot / 2.0;
+  if (P.delay_channels != 1) {  // a model per channel: a fast phasor per channel, exact where undecided
+    for (int j = 0; j < nrun; ++j) {
+      const int c = c0 + j;
+      const float4 d = P.dv[(static_cast<size_t>(c) * P.M + m) * P.A + a];
+      const double ch = static_cast<double>(P.base_ch + c);
+      const float uk = static_cast<float>((ch + half) * fabs(P.k));
+      int wc, ws;
+      if (!q14_fast(d, ch - half, P.k, dt, uk, gq, &wc, &ws)) q14_exact(d, ch, P.ctot, P.ts, dt, P.gain, g, &wc, &ws);
+      o[static_cast<size_t>(j) * words] = (static_cast<uint32_t>(wc) & 0xffffu) | (static_cast<uint32_t>(ws) << 16);
+    }
+    return;
+  }
+  const float4 d = P.dv[static_cast<size_t>(m) * P.A + a];
+  const double tau = fma(static_cast<double>(d.y), dt, static_cast<double>(d.x));
+  const double phi = fma(static_cast<double>(d.w), dt, static_cast<double>(d.z));
+  // the guard's validated range (bf_phase.hpp kQ14MaxMag), at the run's largest |channel| (NaN fails it too)
+  const double ch_last = static_cast<double>(P.base_ch + c0 + nrun - 1);
+  const float mag = fabsf(static_cast<float>(tau)) * static_cast<float>((ch_last + half) * fabs(P.k)) +
+                    fabsf(static_cast<float>(phi));
+  const bool in_range = mag < kQ14MaxMag;
+  double re = 1.0, im = 0.0, cd = 1.0, sd = 0.0;
+  if (in_range) {
+    const double ch0 = static_cast<double>(P.base_ch + c0);
+    sincos_pio2(fma(tau * (ch0 - half), P.k, phi), &im, &re);  // the anchor: rot(c0), as q14_fast forms it
+    sincos_pio2(tau * P.k, &sd, &cd);                          // one channel's rotation
+  }
+  for (int j = 0; j < nrun; ++j) {
+    bool ok = in_range;
+    int wc = q14_pair(re, gq, &ok), ws = q14_pair(im, gq, &ok);
+    if (!ok) q14_exact(d, static_cast<double>(P.base_ch + c0 + j), P.ctot, P.ts, dt, P.gain, g, &wc, &ws);
+    o[static_cast<size_t>(j) * words] = (static_cast<uint32_t>(wc) & 0xffffu) | (static_cast<uint32_t>(ws) << 16);
+    const double r2 = fma(re, cd, -im * sd);
+    im = fma(re, sd, im * cd);
+    re = r2;
+  }
+}
+
+}  // namespace
+
+int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t st) {
+  Q14TableArgs Q{};
+  Q.dv = P.dv;
+  Q.gain = P.gain;
+  Q.out = out;
+  Q.delay_channels = P.delay_channels;
+  Q.B = P.B, Q.C = P.C, Q.A = P.A, Q.M = P.M;
+  Q.Sp = w32_table_steps(P.A);
+  Q.nslabs = (P.M + 31) / 32;
+  Q.layout = layout;
+  Q.base_ch = P.base_ch;
+  Q.ctot = P.ctot, Q.ts = P.ts, Q.k = P.k, Q.t0 = P.t0, Q.batch_dt = P.batch_dt;
+  const long long words = layout == kLayoutNatural ? static_cast<long long>(P.M) * P.A
+                                                   : 1024LL * Q.Sp * Q.nslabs;
+  const long long gx = (words + 255) / 256, gy = (P.C + kQ14Run - 1) / kQ14Run;
+  BF_REQUIRE(gx < (1LL << 31) && gy < 65536 && P.B < 65536, "q14 table: grid too large");
+  if (P.gain)
+    hipLaunchKernelGGL(q14_table_kernel<true>, dim3(static_cast<unsigned>(gx), static_cast<unsigned>(gy), P.B),
+                       dim3(256), 0, st, Q);
+  else
+    hipLaunchKernelGGL(q14_table_kernel<false>, dim3(static_cast<unsigned>(gx), static_cast<unsigned>(gy), P.B),
+                       dim3(256), 0, st, Q);
+  BF_LAUNCHED("q14_table_kernel");
+}
+
+}  // namespace bf
+
+extern "C" int bf_q14_coeffs(const float* delay_vals, int delay_channels, const float* gains, uint32_t* out, int B,
+                             int C, int A, int M, int Ctot, int xeng_id, double sample_period, double t0,
+                             double batch_dt, void* stream) {
+  BF_REQUIRE(delay_vals && out, "bf_q14_coeffs: null pointer");
+  BF_REQUIRE(B > 0 && C > 0 && A > 0 && M > 0 && Ctot > 0 && xeng_id >= 0,
+             "bf_q14_coeffs: bad shape B=%d C=%d A=%d M=%d Ctot=%d", B, C, A, M, Ctot);
+  BF_REQUIRE(delay_channels == 1 || delay_channels == C, "bf_q14_coeffs: delay_channels must be 1 or C");
+  BF_REQUIRE(sample_period > 0.0, "bf_q14_coeffs: sample_period must be > 0");
+  BF_REQUIRE((reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 3) == 0,
+             "bf_q14_coeffs: misaligned buffer");
+  bf::FusedArgs P{};
+  P.dv = reinterpret_cast<const float4*>(delay_vals);
+  P.gain = gains;
+  P.delay_channels = delay_channels;
+  P.B = B, P.C = C, P.A = A, P.M = M;
+  P.base_ch = static_cast<long long>(C) * xeng_id;
+  P.ctot = static_cast<double>(Ctot);
+  P.ts = sample_period;
+  P.k = -3.141592653589793 / (static_cast<double>(Ctot) * sample_period);
+  P.t0 = t0;
+  P.batch_dt = batch_dt;
+  return bf::launch_q14_table(P, out, bf::kLayoutNatural, bf::as_stream(stream));
+}

@@ -14,6 +14,7 @@
 // (hi << 8) + lo (the item kernel's per-step fold would cost 8 VALU per tile per step here).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "bf_fused.hpp"
 
@@ -355,9 +356,45 @@ int launch_w8(FusedArgs P, hipStream_t st) {
 constexpr int kW32Beams = 32;
 
 // k-steps of 32 antennas padded to a multiple of 4 (the four-buffer rotation); padded steps have zero table rows
-__host__ __device__ inline int w32_steps(int A) { return 4 * ((((A + 31) >> 5) + 3) / 4); }
+__host__ __device__ inline int w32_steps(int A) { return w32_table_steps(A); }
+// LDS: the Q14 limb image (Sp steps x 4 tiles x 2 limbs x 64 lanes x 16 B) + the unsigned correction's partial
+// column sums (4 waves x 64 columns)
 __host__ __device__ inline size_t w32_lds_bytes(int A) {
-  return static_cast<size_t>(w32_steps(A)) * 4 * 2 * 64 * 16 + 4 * 32 * 4;
+  return static_cast<size_t>(w32_steps(A)) * 4 * 2 * 64 * 16 + 4 * 64 * 4;
+}
+
+typedef uint16_t u16x2_t __attribute__((ext_vector_type(2)));
+
+// One table unit -- beam ml of the slab x 8 slot antennas (group g: step g >> 2, lane group g & 3) as 8 words
+// (Wc | Ws << 16) -- into the LDS limb image: 4 entries of 16 bytes, one per (column 2 ml / 2 ml + 1, limb).  Column
+// 2 ml holds (Wc, -Ws) per antenna, column 2 ml + 1 (Ws, Wc); balanced limbs W = 256 hi + lo: lo is W's byte 0, hi
+// byte 1 of W + 128 (16-bit lanes: no carry between the halves).  Per antenna 3 packed 16-bit ops, per antenna
+// pair one v_perm per entry dword.
+__device__ __forceinline__ void w32_expand_unit(int8_t* lb, int ml, int g, const u32x4_t& q0, const u32x4_t& q1) {
+  const uint32_t d[8] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
+  uint32_t n[8], np[8], pp[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const u16x2_t v = __builtin_bit_cast(u16x2_t, d[i]);
+    const u16x2_t neg = v * u16x2_t{1, 0xffff};  // (Wc, -Ws)
+    n[i] = __builtin_bit_cast(uint32_t, neg);
+    np[i] = __builtin_bit_cast(uint32_t, neg + u16x2_t{128, 128});
+    pp[i] = __builtin_bit_cast(uint32_t, v + u16x2_t{128, 128});
+  }
+  u32x4_t e_hi0, e_lo0, e_hi1, e_lo1;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    e_lo0[q] = __builtin_amdgcn_perm(n[2 * q + 1], n[2 * q], 0x06040200u);    // [Wc.b0, -Ws.b0] x 2 antennas
+    e_hi0[q] = __builtin_amdgcn_perm(np[2 * q + 1], np[2 * q], 0x07050301u);  // hi limbs of (Wc, -Ws)
+    e_lo1[q] = __builtin_amdgcn_perm(d[2 * q + 1], d[2 * q], 0x04060002u);    // [Ws.b0, Wc.b0]
+    e_hi1[q] = __builtin_amdgcn_perm(pp[2 * q + 1], pp[2 * q], 0x05070103u);  // hi limbs of (Ws, Wc)
+  }
+  const int st = g >> 2, h = g & 3, tau = ml >> 3, row = (2 * ml) & 15;
+  int8_t* o = lb + ((((st * 4 + tau) * 2) * 64) + row + 16 * h) * 16;  // column 2 ml, limb 0 (= hi)
+  *reinterpret_cast<u32x4_t*>(o) = e_hi0;
+  *reinterpret_cast<u32x4_t*>(o + 64 * 16) = e_lo0;
+  *reinterpret_cast<u32x4_t*>(o + 16) = e_hi1;
+  *reinterpret_cast<u32x4_t*>(o + 16 + 64 * 16) = e_lo1;
 }
 
 // One step's voltages: 8 antennas' 8-byte runs.  (Raw buffer loads with the row offsets as soffsets would save the
@@ -654,7 +691,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               int y = (hi[p][i][t][r] << 8) + lo[p][i][t][r];
-              if constexpr (!Signed) {  // unsigned samples: 128 * the column sum (two wave partials)
+              if constexpr (!Signed) {  // unsigned samples: 128 * the column sum (wave partials)
                 const int cl = 16 * t + 4 * h + r;
                 y += 128 * (partial[(cl >> 5) * 32 + (cl & 31)] + partial[((cl >> 5) + 2) * 32 + (cl & 31)]);
               }
@@ -711,6 +748,261 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
   }
 }
 
+
+// ---- the table-driven 32-beam kernel (the default with a workspace) -----------------------------------------------
+// The Q14 coefficients come from the launch's table (q14_table_kernel, kLayoutW32: per (b, c, slab) 1024 Sp words,
+// thread tid's units j = tid + 256 j as two 16-byte loads each) instead of phasors evaluated here, and a workgroup
+// walks kW32TChannels consecutive channels of its slab: the next channel's table is requested after the current
+// channel's last MFMAs (its latency under the stores), and the voltage prefetch runs on from one channel into the
+// next, so only a workgroup's first channel starts cold (measured on the one-channel form: a cold start -- table +
+// first voltage steps -- per (channel, slab) cost ~50 us of 430 at config 4, profiles/r3_e_w32t_ablation.txt).
+// Mode (diagnostics): 1 no table loads / expansion, 4 no stores, 8 no voltage loads.
+constexpr int kW32TChannels = 4;
+
+// Early: request the next channel's table during the last pass's pol-1 stores (else after the last pass).
+// kSp, kNP: compile-time k-steps and passes (config 4: 8 and 2; 0 = from the shape).  With both known, the channel's
+// 16 steps are straight-line code: the four step buffers keep their registers, and the compiler no longer re-homes
+// them through copies behind s_waitcnt vmcnt(22 .. 0) at every loop header -- a full drain of the voltage prefetch
+// every four steps in the runtime-bounded form.
+template <bool Signed, int Mode = 0, bool Early = true, int kSp = 0, int kNP = 0, int kNB = 4>
+__global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(FusedArgs P) {
+  extern __shared__ __attribute__((aligned(16))) int4 lds4[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const int gpb = (P.C + kW32TChannels - 1) / kW32TChannels;  // channel groups per batch
+  int slab, grp;
+  if (P.xcd_order) {  // the slabs of one channel group back to back on one XCD: the second re-reads from L2
+    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
+    slab = local % P.nslabs;
+    grp = (local / P.nslabs) * 8 + x;
+    if (grp >= P.B * gpb) return;
+  } else {
+    slab = blockIdx.x % P.nslabs;
+    grp = blockIdx.x / P.nslabs;
+  }
+  const int b = grp / gpb, c0 = (grp - b * gpb) * kW32TChannels;
+  const int nk = min(kW32TChannels, P.C - c0);
+  const int m0 = slab * kW32Beams;
+  const int Sp = kSp ? kSp : w32_steps(P.A);
+  const int T2 = P.T >> 1;
+  const int nchunks = (T2 + 15) >> 4;                      // 32-sample chunks
+  const int npasses = kNP ? kNP : (nchunks + 3) >> 2;  // per wave, the same count for every wave
+  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
+  const uint32_t hoff = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride);  // < 24 * stride
+  const uint32_t ch_bytes = static_cast<uint32_t>(P.T) * 4;  // next channel of an antenna row
+  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c0) * static_cast<size_t>(P.T) * 4;
+  int8_t* lb = reinterpret_cast<int8_t*>(lds4);
+  int* partial = reinterpret_cast<int*>(lb + static_cast<size_t>(Sp) * 4 * 2 * 64 * 16);  // [4 waves][64 columns]
+  const u32x4_t* tbase = reinterpret_cast<const u32x4_t*>(P.table) +
+                         ((static_cast<size_t>(b) * P.C + c0) * P.nslabs + slab) * 256 * Sp;
+  const size_t tstride = static_cast<size_t>(P.nslabs) * 256 * Sp;  // u32x4 per channel
+
+  // the voltage prefetch: step ls of pass lp of channel lk next, across the workgroup's channels
+  __builtin_assume(Sp >= 4 && (Sp & 3) == 0 && npasses >= 1 && nk >= 1);
+  const int total = nk * npasses * Sp;
+  int issued = 0, ls = 0, lp = 0, lk = 0;
+  auto issue = [&](u32x2_t (&d)[8]) {
+    const uint32_t loff = hoff + static_cast<uint32_t>(lk) * ch_bytes +
+                          static_cast<uint32_t>(min((wave + 4 * lp) * 16 + tl, T2 - 1)) * 8u;
+    w32_load<Mode>(base, ant_stride, loff, ls, P.A, d);
+    ++issued;  // selects, not branches (see the one-channel kernel); past the last step it repeats that step
+    const bool adv = issued < total;
+    const bool wrap = ls + 1 == Sp, pwrap = lp + 1 == npasses;
+    ls = adv ? (wrap ? 0 : ls + 1) : ls;
+    lp = (adv && wrap) ? (pwrap ? 0 : lp + 1) : lp;
+    lk = (adv && wrap && pwrap) ? lk + 1 : lk;
+  };
+  u32x4_t tq[4][2];  // this thread's table units of the channel being staged
+  auto load_table = [&](int kc) {
+    if constexpr ((Mode & 1) == 0) {
+      // a buffer resource on the channel's (uniform) table block + 32-bit lane offsets: no 64-bit per-lane pointers
+      // (hoisted out of the channel loop they were spilled)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<u32x4_t*>(tbase + static_cast<size_t>(kc) * tstride), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // Sp / 2 units (4 or 2); unconditional loads (clamped unit)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+          tq[j][hf] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rs, static_cast<uint32_t>(((min(j, Sp / 2 - 1) * 2 + hf) * 256 + tid) * 16), 0, 0));
+    }
+  };
+  load_table(0);
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr int NB = kSp ? kNB : 4;  // step buffers (NB - 1 steps in flight while one is contracted)
+  u32x2_t db[NB][8];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) issue(db[j]);
+  __builtin_amdgcn_sched_barrier(0);
+
+  const float s32 = P.out_scale * 0x1p-14f;
+  const int M2 = 2 * P.M;
+  const bool full = m0 + kW32Beams <= P.M && (M2 & 15) == 0;  // 16-byte row pieces (uniform)
+  for (int kc = 0; kc < nk; ++kc) {
+    const int c = c0 + kc;
+    if constexpr ((Mode & 1) == 0) {  // the channel's table -> LDS limb image (+ unsigned column sums)
+      const int ml = tid & 31;
+      int cs0 = 0, cs1 = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (2 * j >= Sp) break;  // uniform
+        w32_expand_unit(lb, ml, (tid >> 5) + 8 * j, tq[j][0], tq[j][1]);
+        if constexpr (!Signed) {
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int wc = static_cast<int16_t>(tq[j][hf][q] & 0xffffu), ws = static_cast<int>(tq[j][hf][q]) >> 16;
+              cs0 += wc - ws;
+              cs1 += ws + wc;
+            }
+        }
+      }
+      if constexpr (!Signed) {  // + the other half-wave's antennas; one partial per wave and column
+        cs0 += __shfl_xor(cs0, 32);
+        cs1 += __shfl_xor(cs1, 32);
+        if (lane < 32) {
+          partial[wave * 64 + 2 * ml] = cs0;
+          partial[wave * 64 + 2 * ml + 1] = cs1;
+        }
+      }
+    }
+    lds_barrier();  // the image is complete; the voltage prefetch stays in flight
+    if constexpr (!Signed) {  // the four waves' partials -> one total per column
+      if (tid < 64) partial[tid] += partial[64 + tid] + partial[128 + tid] + partial[192 + tid];
+      lds_barrier();
+    }
+    // the passes; the last one is peeled so that the next channel's table registers are never live across an MFMA
+    // loop (a conditional request inside the loop kept them live through every pass: 188 B/lane of spills)
+    auto run_pass = [&](int pass, auto last) {
+      constexpr bool kLast = decltype(last)::value;
+      const int tq2 = (wave + 4 * pass) * 16 + tl;  // sample pair
+      i32x4_t hi[2][2][4], lo[2][2][4];
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) hi[p][i][t] = lo[p][i][t] = i32x4_t{0, 0, 0, 0};
+      if constexpr (kSp != 0) {
+        // straight-line: step g of the channel contracts buffer g % NB (compile-time), scheduling barriers keep each
+        // step's refill after its fragments
+#pragma unroll
+        for (int s = 0; s < kSp; ++s) {
+          constexpr int dummy = 0;
+          (void)dummy;
+          i32x4_t f[2][2];
+          const int j = (pass * kSp + s) % NB;
+          w32_frags<Signed>(db[j], f);
+          __builtin_amdgcn_sched_barrier(0);
+          issue(db[j]);
+          w32_mfma<0>(lds4, s, lane, f, hi, lo);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        for (int s = 0; s < Sp; s += 4) {
+          i32x4_t f[2][2];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            w32_frags<Signed>(db[j], f);
+            issue(db[j]);
+            w32_mfma<0>(lds4, s + j, lane, f, hi, lo);
+          }
+        }
+      }
+      // unconditional in the last pass (the workgroup's last channel re-reads its own table, from L2): with a
+      // conditional request the previous table's registers stayed live through every pass (phi at the back-edge)
+      constexpr bool next_table = kLast && Early;
+      if constexpr (Mode & 4) {
+        if constexpr (next_table) load_table(min(kc + 1, nk - 1));
+        int sum = 0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) sum += hi[p][i][t][0] ^ lo[p][i][t][3];
+        if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[tid] = sum;
+      } else {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          // the next channel's table, requested once pol 0's accumulators are dead (registers) -- its latency runs
+          // under pol 1's stores and the barrier
+          if constexpr (next_table)
+            if (p == 1) {  // pinned: scheduled earlier, the loads overlapped pol 0's accumulators (spills)
+              __builtin_amdgcn_sched_barrier(0);
+              load_table(min(kc + 1, nk - 1));
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          uint32_t pk[2][4];  // [sample i][tile t] -> 4 packed int8 columns 16 t + 4 h + r
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              uint32_t qb[4];
+              int4 cs = int4{0, 0, 0, 0};  // unsigned: the 4 columns' sums, one 16-byte LDS read
+              if constexpr (!Signed) cs = reinterpret_cast<const int4*>(partial)[4 * t + h];
+              const int csr[4] = {cs.x, cs.y, cs.z, cs.w};
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                int y = (hi[p][i][t][r] << 8) + lo[p][i][t][r];
+                if constexpr (!Signed) y += 128 * csr[r];
+                qb[r] = requant_bits(y, s32);
+              }
+              pk[i][t] = pack_low_bytes(qb[0], qb[1], qb[2], qb[3]);
+            }
+          const size_t prow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T);
+          if (full) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) transpose_rows4(pk[i]);
+            if (tq2 < T2) {
+#pragma unroll
+              for (int i = 0; i < 2; ++i) {
+                int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 2 * tq2 + i) * M2 + 2 * m0 + 16 * h;
+                *reinterpret_cast<u32x4_t*>(o) = u32x4_t{pk[i][0], pk[i][1], pk[i][2], pk[i][3]};
+              }
+            }
+          } else if (tq2 < T2) {  // partial slab / unaligned rows: byte stores with the beam guard
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 2 * tq2 + i) * M2 + 2 * m0;
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const int col = 16 * t + 4 * h + r;
+                  if (2 * m0 + col < M2) o[col] = static_cast<int8_t>((pk[i][t] >> (8 * r)) & 255);
+                }
+            }
+          }
+        }
+      }
+    };
+    if constexpr (Early) {
+#pragma unroll
+      for (int pass = 0; pass + 1 < npasses; ++pass) run_pass(pass, std::false_type{});
+      run_pass(npasses - 1, std::true_type{});
+    } else {
+#pragma unroll
+      for (int pass = 0; pass < npasses; ++pass) run_pass(pass, std::false_type{});
+      load_table(min(kc + 1, nk - 1));
+    }
+    if constexpr (kSp != 0 && (kSp * kNP) % NB != 0) {  // re-align the ring: the next channel starts at buffer 0
+      constexpr int r = (kSp * kNP) % NB;
+      u32x2_t tmp[NB][8];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tmp[j][q] = db[(j + r) % NB][q];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) db[j][q] = tmp[j][q];
+    }
+    if (kc + 1 < nk) lds_barrier();  // every wave is done with this image (MFMAs) and column sums (stores)
+  }
+}
+
 template <bool Signed, int Mode = 0>
 int launch_w32(FusedArgs P, hipStream_t st) {
   const size_t lds = w32_lds_bytes(P.A);
@@ -720,6 +1012,21 @@ int launch_w32(FusedArgs P, hipStream_t st) {
   const long long items = static_cast<long long>(P.B) * P.C;
   const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
+  if (P.table && w32_table_fits(P.A) && P.table_bytes >= w32_table_bytes(P.B, P.C, P.A, P.M)) {
+    // the coefficient table of this launch, written by q14_table_kernel just before on `st`
+    const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32, st);
+    if (e != BF_OK) return e;
+    const long long groups = static_cast<long long>(P.B) * ((P.C + kW32TChannels - 1) / kW32TChannels);
+    const long long tgrid = P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs;
+    const int npasses = ((((P.T >> 1) + 15) >> 4) + 3) >> 2;
+    if (w32_steps(P.A) == 8 && npasses == 2)  // config 4's shape: the straight-line 3-buffer ring (386 vs 403 us)
+      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false, 8, 2, 3>),
+                         dim3(static_cast<unsigned>(tgrid)), dim3(kW8Threads), lds, st, P);
+    else
+      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false>), dim3(static_cast<unsigned>(tgrid)),
+                         dim3(kW8Threads), lds, st, P);
+    BF_LAUNCHED("beamform_fused_i8_w32t_kernel");
+  }
   if (P.gain)
     hipLaunchKernelGGL((beamform_fused_i8_w32_kernel<Signed, Mode, true>), dim3(static_cast<unsigned>(grid)),
                        dim3(kW8Threads), lds, st, P);
@@ -784,6 +1091,43 @@ extern "C" int bf_diag_w32_stamps(const uint8_t* raw, const float* dv, void* y, 
   hipLaunchKernelGGL((bf::beamform_fused_i8_w32_kernel<true, 128, false>), dim3(static_cast<unsigned>(grid)),
                      dim3(bf::kW8Threads), bf::w32_lds_bytes(A), bf::as_stream(stream), P);
   BF_LAUNCHED("beamform_fused_i8_w32_kernel");
+}
+
+// The table-driven 32-beam kernel alone (the table made once, outside the timing): mode = the kernel's Mode bits
+// (1: no table loads / expansion, 2 no MFMA, 4 no stores, 8 no voltage loads); mode -1 = the table generator alone.
+extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, void* y, void* table, int B, int C,
+                                 int T, int A, int M, int Ctot, double ts, void* stream) {
+  bf::FusedArgs P{};
+  P.raw = raw;
+  P.dv = reinterpret_cast<const float4*>(dv);
+  P.y = y;
+  P.table = static_cast<const uint32_t*>(table);
+  P.table_bytes = bf::w32_table_bytes(B, C, A, M);
+  P.delay_channels = 1;
+  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
+  P.ctot = Ctot;
+  P.ts = ts;
+  P.k = -3.141592653589793 / (Ctot * ts);
+  P.batch_dt = 1e-3;
+  P.out_scale = 1.0f / 64;
+  P.nslabs = (M + 31) / 32;
+  P.xcd_order = P.nslabs > 1;
+  hipStream_t st = bf::as_stream(stream);
+  if (mode < 0) return bf::launch_q14_table(P, static_cast<uint32_t*>(table), bf::kLayoutW32, st);
+  const long long groups = static_cast<long long>(B) * ((C + bf::kW32TChannels - 1) / bf::kW32TChannels);
+  const unsigned grid = static_cast<unsigned>(P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs);
+  const size_t lds = bf::w32_lds_bytes(A);
+#define BF_W32T(m) \
+  case m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 100 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 300 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 400 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 4>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break
+  switch (mode) {
+    BF_W32T(0); BF_W32T(1); BF_W32T(4); BF_W32T(8); BF_W32T(9); BF_W32T(12);
+    default: return BF_ERR_ARG;
+  }
+#undef BF_W32T
+  BF_LAUNCHED("beamform_fused_i8_w32t_kernel");
 }
 
 extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y, int B, int C, int T, int A, int M,

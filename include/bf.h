@@ -151,6 +151,27 @@ int bf_beamform_fused_weighted(const uint8_t* raw, const float* delay_vals, int 
                                double sample_period, double t0, double batch_dt, int flags, float out_scale,
                                void* stream);
 
+/* bf_beamform_fused_weighted with a caller-owned device workspace (the fused call itself never allocates).  With at
+ * least bf_fused_workspace_bytes(...) bytes, the int8 beams of many antennas x beams (config 4: the 32-beam integer
+ * kernel) take their Q14 coefficients from a table that bf_q14_coeffs' kernel writes into the workspace just before,
+ * on `stream` -- the wavefront-parallel phasor generator of the reference's two-kernel structure (coeff_generator.py
+ * then matrix_multiply.py; BeamformerKernels.cu:7-189), one float64 complex multiply per coefficient along the
+ * channels -- instead of evaluating every phasor inside the contraction kernel.  Same contract, same bits; workspace
+ * NULL (or too small) = bf_beamform_fused_weighted.  bf_fused_workspace_bytes gives 0 for shapes and flags that use
+ * no workspace.  The workspace must be 16-byte aligned and must not be shared by calls in flight on other streams. */
+int bf_fused_workspace_bytes(int B, int C, int T, int A, int M, int flags, size_t* bytes);
+int bf_beamform_fused_ws(const uint8_t* raw, const float* delay_vals, int delay_channels, const float* gains, void* y,
+                         int B, int C, int T, int A, int M, int Ctot, int xeng_id, double sample_period, double t0,
+                         double batch_dt, int flags, float out_scale, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* The int8 path's steering coefficients (the Q14 integer contract, oracle quantise_coeffs of fused_tables):
+ *   out[b][c][m][a] = (uint16)Wc | (uint32)Ws << 16, Wc = rne(2^14 * RN32(g * RN32(cos rot))), Ws the same for sin,
+ *   rot the reference's float64 phase (coeff_generator_cpu.py:145-164) of channel c + C * xeng_id at
+ *   dt = t0 + b * batch_dt (SURVEY A3 time extension), g = gains[m][a] (NULL = 1).  delay_vals f32 (Cd, M, A, 4). */
+int bf_q14_coeffs(const float* delay_vals, int delay_channels, const float* gains, uint32_t* out, int B, int C, int A,
+                  int M, int Ctot, int xeng_id, double sample_period, double t0, double batch_dt, void* stream);
+
 /* 8-bit requantiser (no reference counterpart; SURVEY §7 build step 7): q = clamp(rne(y*scale), -127, 127). */
 int bf_requant(const float* y, int8_t* q, size_t n, float scale, void* stream);
 

@@ -47,6 +47,14 @@ def random_delays(C, M, A, seed, rates=True):
     return d
 
 
+def i8_path(name):
+    """FusedBeamformerTemplate kernel options of an int8 test path: the kernel path, plus "wide-inkernel" = the
+    32-beam int8 kernel evaluating its phasors itself (no generated coefficient table)."""
+    if name == "wide-inkernel":
+        return dict(kernel_path="wide", coeff_table=False)
+    return dict(kernel_path=name)
+
+
 def run(op, queue, inputs, outputs):
     op.ensure_all_bound()
     for name, host in inputs.items():
@@ -350,7 +358,7 @@ def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C
     (4, 1, 16, 1024, 1, 16, True), (80, 24, 3, 16, 3, 1, True), (32, 8, 4, 64, 2, 1, False),
     (48, 12, 2, 128, 2, 1, False), (33, 5, 3, 80, 2, 3, True), (16, 8, 3, 48, 2, 1, True),
     (64, 16, 2, 112, 1, 1, False), (40, 32, 2, 64, 1, 2, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel", "wide16"])
 def test_fused_int8_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """int8 (requantised) beams: the integer MFMA path reproduces the oracle's integer contract bit for bit, on the
     item kernel (A <= 64, T <= 256; others fall through to generic) and the generic kernel (any A, T)."""
@@ -363,7 +371,7 @@ def test_fused_int8_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, 
     for scale in (1.0 / 64, 1.0 / 16):
         op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=dch, sample_signed=signed,
                                      out_int8=True, out_scale=scale, t0=t0, batch_dt=bdt,
-                                     kernel_path=i8_kernel).instantiate(command_queue)
+                                     **i8_path(i8_kernel)).instantiate(command_queue)
         (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
         ref = O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, scale=scale, signed=signed)
         assert q.dtype == np.int8
@@ -487,7 +495,7 @@ def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, 
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
     (64, 16, 3, 256, 2, 1, True), (64, 16, 2, 256, 2, 1, False), (19, 3, 4, 48, 2, 4, False),
     (130, 9, 2, 64, 1, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel", "wide16"])
 def test_fused_int8_beam_weights_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """Weighted int8 beams: Q14 limbs of the weighted float32 coefficients, bit-exact to the integer contract."""
     Ctot, xeng, t0, bdt = 4096, 2, 1e-3, 256 * 8192 * TS
@@ -499,7 +507,7 @@ def test_fused_int8_beam_weights_bit_exact(context, command_queue, i8_kernel, A,
     g = rng.uniform(-1.9, 1.9, (M, A)).astype(np.float32)
     op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=dch, sample_signed=signed,
                                  out_int8=True, out_scale=1 / 64, t0=t0, batch_dt=bdt,
-                                 beam_weights=True, kernel_path=i8_kernel).instantiate(command_queue)
+                                 beam_weights=True, **i8_path(i8_kernel)).instantiate(command_queue)
     for m in range(M):
         op.set_beam_weights(m, g[m])
     (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
@@ -526,7 +534,7 @@ def boundary_delays(M, A, seed):
 
 @pytest.mark.parametrize("A,M,C,T,B,signed", [(64, 16, 3, 256, 2, True), (64, 16, 2, 256, 2, False),
                                               (19, 3, 3, 48, 2, False), (256, 64, 1, 32, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide16"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel", "wide16"])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_fused_int8_rounding_boundaries(context, command_queue, i8_kernel, weighted, A, M, C, T, B,
                                         signed):
@@ -541,7 +549,7 @@ def test_fused_int8_rounding_boundaries(context, command_queue, i8_kernel, weigh
     g = rng.choice(np.float32([1.0, 0.5, -1.0, 0.75]), (M, A)).astype(np.float32) if weighted else None
     op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=signed,
                                  out_int8=True, out_scale=1 / 64, t0=t0, batch_dt=bdt,
-                                 beam_weights=weighted, kernel_path=i8_kernel).instantiate(command_queue)
+                                 beam_weights=weighted, **i8_path(i8_kernel)).instantiate(command_queue)
     if weighted:
         for m in range(M):
             op.set_beam_weights(m, g[m])

@@ -73,6 +73,30 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
             ts = sorted(res[mode])
             print(f"  wide tw={tw} mode {mode:2d} {wnames[mode]:18s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
                   f"alg {alg / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
+if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam int8 kernel alone (+ its generator)
+    lib.bf_diag_w32_table.argtypes = [I, V, V, V, V, I, I, I, I, I, I, D, V]
+    Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
+    tb = accel.DeviceArray(ctx, (B * C * ((M + 31) // 32) * 1024 * 8 + 4096,), np.uint32)
+    assert lib.bf_diag_w32_table(-1, bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, tb.ptr, B, C, T, A, M, Ctot, 1 / 1712e6,
+                                 q.handle) == 0
+    tnames = {-1: "generator only", 0: "full (early table)", 1: "no table", 4: "no-store", 8: "no-load",
+              9: "no table,no-load", 12: "no-store,no-load"}
+    base = {m: v for m, v in tnames.items() if m >= 0}
+    tnames.update({100 + m: v.replace("early", "late") + (" (late)" if m else "") for m, v in base.items()})
+    tnames.update({300 + m: v.replace("early ", "") + " [unrolled NB3]" for m, v in base.items()})
+    tnames.update({400 + m: v.replace("early ", "") + " [unrolled NB4]" for m, v in base.items()})
+    if _os.environ.get("W32T_MODES"):
+        tnames = {int(m): tnames.get(int(m), str(m)) for m in _os.environ["W32T_MODES"].split(",")}
+    alg8 = nin + nout // 4
+    res = {m: [] for m in tnames}
+    for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
+        for mode in tnames:
+            res[mode].append(timeit(lambda i: lib.bf_diag_w32_table(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
+                                                                    tb.ptr, B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
+    for mode in tnames:
+        ts = sorted(res[mode])
+        print(f"  w32t mode {mode:3d} {tnames[mode]:28s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
+              f"alg {alg8 / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
 if "w8" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_w8.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
     w8names = {0: "full (fast+fixup)", 128: "exact-only coef", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
