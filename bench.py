@@ -509,13 +509,17 @@ def mfma_util(wl, out_int8, int8_contract, kernel_s):
             "issued": round(issued / kernel_s / 1e12, 1), "frac_issued": round(issued / kernel_s / 1e12 / peak, 4)}
 
 
-def kernel_name(wl, out_int8, int8_contract="q14"):
+def kernel_name(wl, out_int8, int8_contract="q14", coeff_table="on"):
     """The launch's dominant kernel (bf_fused.hip dispatch): item kernels for A <= 64 and T <= 256, else the wide
-    kernels."""
+    kernels; the int8 32-beam path with a coefficient table (A <= 256) is the table-driven contraction, after its
+    generator (q14_table_kernel, reported per step beside it)."""
     integer = out_int8 and int8_contract == "q14"
     if wl["A"] <= 64 and wl["T"] <= 256:
         return "beamform_fused_i8_item_kernel" if integer else "beamform_fused_item_kernel"
-    return "beamform_fused_i8_w32_kernel" if integer else "beamform_fused_wide_kernel"
+    if integer:
+        return "beamform_fused_i8_w32t_kernel" if coeff_table == "on" and wl["A"] <= 256 else \
+            "beamform_fused_i8_w32_kernel"
+    return "beamform_fused_wide_kernel"
 
 
 def secondary(args, dist, workload, out_int8, int8_contract="q14"):
@@ -527,7 +531,7 @@ def secondary(args, dist, workload, out_int8, int8_contract="q14"):
     out = {"workload": workload + ": " + wl["desc"],
            "output": ("int8" + ("" if int8_contract == "q14" else " (requantised from float32 beams)"))
            if out_int8 else "float32",
-           "kernel": kernel_name(wl, out_int8, int8_contract),
+           "kernel": kernel_name(wl, out_int8, int8_contract, args.coeff_table),
            "value": round(r["samples_per_step"] * args.steps * dist.world / r["t_max"] / 1e9, 2),
            "unit": "Gsamples/s", "n_gpus": dist.world,
            "roofline_frac": round(r["alg_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
@@ -590,7 +594,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "read_frac": round(r["read_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
-                     "kernel": kernel_name(wl, args.out_int8, args.int8_contract),
+                     "kernel": kernel_name(wl, args.out_int8, args.int8_contract, args.coeff_table),
                      "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"],
                      "read_bytes_per_launch": r["read_bytes"]},
         "mfma": mfma_util(wl, args.out_int8, args.int8_contract, r["kernel_s"]),

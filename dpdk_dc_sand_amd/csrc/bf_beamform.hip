@@ -367,6 +367,13 @@ __global__ __launch_bounds__(kThreads, 2) void beamform_table_persist_kernel(
   };
   float tv[UPT][8];
   auto table_load = [&](int slab, size_t bpc) {
+    if constexpr (Mode & 16) {  // diagnostics: no table loads
+#pragma unroll
+      for (int u = 0; u < UPT; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tv[u][j] = 1e-3f * static_cast<float>(j + u + slab);
+      return;
+    }
     const float* wp = w + bpc * static_cast<size_t>(K2) * M2;
     const int tau0 = slab * NTS;
     // rows past 2A only occur as whole 8-row units (A % 8 == 0): clamp the unit's first row, zeroed at the store
@@ -490,8 +497,13 @@ __global__ __launch_bounds__(kThreads, 2) void beamform_table_persist_kernel(
         if (j >= nrg) break;
         float* orow = yp + static_cast<size_t>((wave + kWaves * j) * kSamplesPerBlock + tl) * M2;
 #pragma unroll
-        for (int tau = 0; tau < NTS; ++tau)
-          if (tau < nts) store_f32<NTS>(orow, 16 * (tau0 + tau) + 4 * h, M2, acc[g][tau]);
+        for (int tau = 0; tau < NTS; ++tau) {
+          if constexpr (Mode & 4) {
+            if (acc[g][tau][0] == 1234.5f) orow[tau] = acc[g][tau][1];
+          } else {
+            if (tau < nts) store_f32<NTS>(orow, 16 * (tau0 + tau) + 4 * h, M2, acc[g][tau]);
+          }
+        }
       }
       // rows of pair pi + 2: this item's, or (past its last pair) the next item's first pairs
 #pragma unroll
@@ -655,8 +667,16 @@ extern "C" int bf_diag_table(int mode, int nts, const uint8_t* x, const float* w
     BF_TABLE_MODE(9);
     BF_TABLE_MODE(6);
     BF_TABLE_MODE(7);
-    case 200:  // the persistent form (A/B against mode 0)
+    case 200:  // the persistent form (A/B against mode 0); 200 + Mode bits: 1 no LDS staging, 4 no stores,
+               // 8 no x loads, 16 no table loads
       return nts == 2 ? bf::launch_persist<true, 2, 16, 8>(x, w, y, bpc, NB, A, M, S, NT, st) : BF_ERR_ARG;
+    case 201: return bf::launch_persist<true, 2, 16, 8, 1>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 204: return bf::launch_persist<true, 2, 16, 8, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 208: return bf::launch_persist<true, 2, 16, 8, 8>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 216: return bf::launch_persist<true, 2, 16, 8, 16>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 217: return bf::launch_persist<true, 2, 16, 8, 17>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 220: return bf::launch_persist<true, 2, 16, 8, 20>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 228: return bf::launch_persist<true, 2, 16, 8, 28>(x, w, y, bpc, NB, A, M, S, NT, st);
     case 300:  // the non-persistent 16-byte ring
       return nts == 4 ? bf::launch_ring<true, 4, 16>(x, w, y, bpc, NB, A, M, S, NT, st)
                       : bf::launch_ring<true, 2, 16>(x, w, y, bpc, NB, A, M, S, NT, st);

@@ -85,6 +85,59 @@ __global__ __launch_bounds__(256) void coeff_gen_tile_kernel(const float4* __res
   }
 }
 
+// Block form (the default): one workgroup per (c, run of na antennas).  The run's 2 na rows of a (2A, 2M) plane are
+// ONE contiguous 16 na M-byte piece of every (b, p) plane, so the workgroup evaluates its na M phasors once (model
+// rows read antenna-fastest, coalesced), lays the piece out in LDS (one 16-byte pad per antenna pair of rows), and
+// then streams it to the B P planes with 16-byte stores -- whole contiguous runs, no partial lines (the per-(a, m)
+// kernels above store 8-byte pairs into rows 2M floats apart).  Cache & 2: non-temporal stores (the table is
+// written once and read by the multiply much later).
+constexpr int kCoefBlockLds = 32 * 1024;
+__host__ __device__ inline int coef_block_ants(int A, int M) {
+  int na = kCoefBlockLds / 16 / (M + 1);
+  if (na >= 16) na &= ~15;
+  return na < A ? na : A;
+}
+
+template <int Cache>
+__global__ __launch_bounds__(256) void coeff_gen_block_kernel(const float4* __restrict__ dv, float* __restrict__ out,
+                                                              int BP, int C, int A, int M, int na, long long base_ch,
+                                                              double ctot, double ts) {
+  extern __shared__ __attribute__((aligned(16))) float4 img4[];  // [antenna][M + 1] float4 (rows 2a, 2a + 1 + pad)
+  float* img = reinterpret_cast<float*>(img4);
+  const int c = static_cast<int>(blockIdx.y);
+  const int a0 = static_cast<int>(blockIdx.x) * na;
+  const int nb = min(na, A - a0);
+  const int pitch = 4 * (M + 1);  // floats per antenna
+  const PhaseK k = make_phase(ctot, ts);
+  const double ch = static_cast<double>(base_ch + c);
+  for (int e = static_cast<int>(threadIdx.x); e < nb * M; e += 256) {
+    const int m = e / nb, la = e - m * nb;
+    const float4 d = dv[(static_cast<size_t>(c) * M + m) * A + a0 + la];  // delay_vals[c][m][a]
+    float re, im;
+    steering_coeff(d, ch, k, 0.0, &re, &im);
+    float* r = img + la * pitch + 2 * m;
+    *reinterpret_cast<float2*>(r) = make_float2(re, im);           // W[2a][2m], W[2a][2m+1]
+    *reinterpret_cast<float2*>(r + 2 * M) = make_float2(-im, re);  // W[2a+1][2m], W[2a+1][2m+1]
+  }
+  __syncthreads();
+  const size_t plane = static_cast<size_t>(2 * A) * (2 * M);
+  const size_t bp_stride = static_cast<size_t>(C) * plane;
+  float4* dst = reinterpret_cast<float4*>(out + static_cast<size_t>(c) * plane + static_cast<size_t>(2 * a0) * (2 * M));
+  for (int j = static_cast<int>(threadIdx.x); j < nb * M; j += 256) {  // 16-byte pieces of the run
+    const int la = j / M;
+    const float4 v = img4[la * (M + 1) + (j - la * M)];
+    for (int bp = 0; bp < BP; ++bp) {
+      float4* o = dst + static_cast<size_t>(bp) * (bp_stride >> 2) + j;
+      if constexpr (Cache & 2) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(o));
+      } else {
+        *o = v;
+      }
+    }
+  }
+}
+
 template <bool F16>
 __global__ __launch_bounds__(256) void coeff_gen_time_kernel(const float4* __restrict__ dv, int delay_channels,
                                                              void* __restrict__ out, int n_times, int C, int A, int M,
@@ -128,7 +181,25 @@ extern "C" int bf_coeff_gen(const float* delay_vals, float* out, int B, int P, i
   BF_REQUIRE((reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0,
              "bf_coeff_gen: misaligned buffer");
   BF_REQUIRE(static_cast<long long>(A) * M < (1LL << 31) && C < 65536, "bf_coeff_gen: shape too large");
-  if (A >= 32 && M >= 32) {  // many antennas and beams: the tiled, coalesced-read form
+  const char* form = bf::diag_env("BF_COEFF_FORM");  // measurement: "thread" / "tile" = the per-(a, m) kernels
+  const int na = bf::coef_block_ants(A, M);
+  if (!form && na >= 1) {
+    const unsigned gx = static_cast<unsigned>((A + na - 1) / na);
+    const size_t lds = static_cast<size_t>(na) * (M + 1) * 16;
+    const char* nt = bf::diag_env("BF_COEFF_NT");
+    const auto dv = reinterpret_cast<const float4*>(delay_vals);
+    const long long base = static_cast<long long>(C) * xeng_id;
+    if (nt && nt[0] == '0')
+      hipLaunchKernelGGL(bf::coeff_gen_block_kernel<0>, dim3(gx, static_cast<unsigned>(C)), dim3(256), lds,
+                         bf::as_stream(stream), dv, out, B * P, C, A, M, na, base, static_cast<double>(Ctot),
+                         sample_period);
+    else
+      hipLaunchKernelGGL(bf::coeff_gen_block_kernel<2>, dim3(gx, static_cast<unsigned>(C)), dim3(256), lds,
+                         bf::as_stream(stream), dv, out, B * P, C, A, M, na, base, static_cast<double>(Ctot),
+                         sample_period);
+    BF_LAUNCHED("coeff_gen_block_kernel");
+  }
+  if (A >= 32 && M >= 32 && !(form && form[0] == 't' && form[1] == 'h')) {  // many antennas and beams: the tiled, coalesced-read form
     const unsigned gx = static_cast<unsigned>(((A + bf::kCoefTile - 1) / bf::kCoefTile) *
                                               ((M + bf::kCoefTile - 1) / bf::kCoefTile));
     hipLaunchKernelGGL(bf::coeff_gen_tile_kernel, dim3(gx, static_cast<unsigned>(C)), dim3(256), 0,

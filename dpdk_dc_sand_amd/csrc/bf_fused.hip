@@ -1187,13 +1187,16 @@ int dispatch(FusedArgs P, hipStream_t st) {
     if (wide && wide_fits(P)) return launch_wide<Signed, Exact>(P, st);
   }
   if (small && choice != BF_FUSED_PATH_GENERIC) {
+    // int8 beams from the float path: bounded to 4 waves per SIMD (124 VGPRs, no spills; cfg3 489 -> 465 us,
+    // profiles/r3_i_cfg3_f32contract_ablation.txt); float32 beams keep the unbounded form (816 vs 811 us)
+    constexpr int kOcc = OutI8 ? 4 : 1;
     const int M2 = 2 * P.M;
     if (P.NT >= 2) {
-      if (M2 % 32 == 0) return launch_item<Signed, OutI8, 2, Exact, true>(P, st);
-      return launch_item<Signed, OutI8, 2, Exact, false>(P, st);
+      if (M2 % 32 == 0) return launch_item<Signed, OutI8, 2, Exact, true, 0, kOcc>(P, st);
+      return launch_item<Signed, OutI8, 2, Exact, false, 0, kOcc>(P, st);
     }
-    if (M2 == 16) return launch_item<Signed, OutI8, 1, Exact, true>(P, st);
-    return launch_item<Signed, OutI8, 1, Exact, false>(P, st);
+    if (M2 == 16) return launch_item<Signed, OutI8, 1, Exact, true, 0, kOcc>(P, st);
+    return launch_item<Signed, OutI8, 1, Exact, false, 0, kOcc>(P, st);
   }
   const char* wn = diag_env("BF_FUSED_GENERIC_NTS");  // measurement: force the slab width
   const int want = wn ? atoi(wn) : 2;
@@ -1495,6 +1498,21 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
   P.out_scale = 1.0f;
   hipStream_t st = bf::as_stream(stream);
   BF_REQUIRE(P.S <= bf::kGroup && T <= 256 && (2 * M) % 32 == 0, "diag: item-kernel full-tile shapes only");
+  if (mode >= 8192) {  // int8 beams requantised from the float32 path (int8_contract = f32): the float item kernel
+    P.out_scale = 1.0f / 64;
+    switch (mode - 8192) {
+      case 0: return bf::launch_item<true, true, 2, false, true, 0>(P, st);
+      case 1: return bf::launch_item<true, true, 2, false, true, 1>(P, st);
+      case 2: return bf::launch_item<true, true, 2, false, true, 2>(P, st);
+      case 4: return bf::launch_item<true, true, 2, false, true, 4>(P, st);
+      case 5: return bf::launch_item<true, true, 2, false, true, 5>(P, st);
+      case 8: return bf::launch_item<true, true, 2, false, true, 8>(P, st);
+      case 128: return bf::launch_item<true, true, 2, false, true, 128>(P, st);
+      case 64: return bf::launch_item<true, true, 2, false, true, 0, 4>(P, st);
+      case 96: return bf::launch_item<true, true, 2, false, true, 0, 3>(P, st);
+      default: bf::set_error("bad mode"); return BF_ERR_ARG;
+    }
+  }
   if (mode >= 512) {  // integer (int8-output) item kernel
     P.out_scale = 1.0f / 64;
     switch (mode - 512) {

@@ -14,9 +14,12 @@
 
 #include "bf_common.hpp"
 
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
 namespace bf {
 
-template <bool Oct>
+// Cache: bit 1 non-temporal voltage loads, bit 2 non-temporal stores (both streams are touched once).
+template <bool Oct, int Cache>
 __global__ __launch_bounds__(256) void reorder_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                       int A, int C, int T, int TT, int nchunk, int xcd_range) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_u32[];
@@ -44,7 +47,13 @@ __global__ __launch_bounds__(256) void reorder_kernel(const uint8_t* __restrict_
       const int tq = idx - a * quads;
       const size_t src = ((static_cast<size_t>(b) * A + a) * C + c) * static_cast<size_t>(T) * 4 +
                          static_cast<size_t>(t0 + 4 * tq) * 4;
-      v[k] = *reinterpret_cast<const uint4*>(in + src);
+      const uint4* ps = reinterpret_cast<const uint4*>(in + src);
+      if constexpr (Cache & 1) {
+        const u32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(ps));
+        v[k] = make_uint4(t[0], t[1], t[2], t[3]);
+      } else {
+        v[k] = *ps;
+      }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -89,8 +98,13 @@ __global__ __launch_bounds__(256) void reorder_kernel(const uint8_t* __restrict_
       w1.z = __builtin_amdgcn_perm(d[5], d[4], 0x07060302u);
       w1.w = __builtin_amdgcn_perm(d[7], d[6], 0x07060302u);
       const size_t off = (static_cast<size_t>(t) * A + a0) * 2;
-      *reinterpret_cast<uint4*>(dst0 + off) = w0;
-      *reinterpret_cast<uint4*>(dst1 + off) = w1;
+      if constexpr (Cache & 2) {
+        __builtin_nontemporal_store(u32x4_t{w0.x, w0.y, w0.z, w0.w}, reinterpret_cast<u32x4_t*>(dst0 + off));
+        __builtin_nontemporal_store(u32x4_t{w1.x, w1.y, w1.z, w1.w}, reinterpret_cast<u32x4_t*>(dst1 + off));
+      } else {
+        *reinterpret_cast<uint4*>(dst0 + off) = w0;
+        *reinterpret_cast<uint4*>(dst1 + off) = w1;
+      }
     }
   } else {
     const uint16_t* lds_u16 = reinterpret_cast<const uint16_t*>(lds_u32);
@@ -112,13 +126,32 @@ __global__ __launch_bounds__(256) void reorder_kernel(const uint8_t* __restrict_
           }
           w[j] = pair;
         }
-        *reinterpret_cast<uint4*>(dst + static_cast<size_t>(e0) * 2) = make_uint4(w[0], w[1], w[2], w[3]);
+        if constexpr (Cache & 2)
+          __builtin_nontemporal_store(u32x4_t{w[0], w[1], w[2], w[3]},
+                                      reinterpret_cast<u32x4_t*>(dst + static_cast<size_t>(e0) * 2));
+        else
+          *reinterpret_cast<uint4*>(dst + static_cast<size_t>(e0) * 2) = make_uint4(w[0], w[1], w[2], w[3]);
       }
     }
   }
 }
 
+template <bool Oct>
+void launch_reorder(int cache, dim3 grid, size_t lds, hipStream_t st, const uint8_t* in, uint8_t* out, int A, int C,
+                    int T, int TT, int nchunk, int xcd_range) {
+  switch (cache) {
+    case 0: hipLaunchKernelGGL((reorder_kernel<Oct, 0>), grid, dim3(256), lds, st, in, out, A, C, T, TT, nchunk, xcd_range); break;
+    case 1: hipLaunchKernelGGL((reorder_kernel<Oct, 1>), grid, dim3(256), lds, st, in, out, A, C, T, TT, nchunk, xcd_range); break;
+    case 2: hipLaunchKernelGGL((reorder_kernel<Oct, 2>), grid, dim3(256), lds, st, in, out, A, C, T, TT, nchunk, xcd_range); break;
+    default: hipLaunchKernelGGL((reorder_kernel<Oct, 3>), grid, dim3(256), lds, st, in, out, A, C, T, TT, nchunk, xcd_range); break;
+  }
+}
+
 }  // namespace bf
+
+namespace {
+constexpr int kReorderCache = 0;  // the product's cache policy (see launch_reorder)
+}
 
 extern "C" int bf_reorder(const uint8_t* in, uint8_t* out, int B, int A, int C, int T, void* stream) {
   BF_REQUIRE(in && out, "bf_reorder: null pointer");
@@ -128,8 +161,10 @@ extern "C" int bf_reorder(const uint8_t* in, uint8_t* out, int B, int A, int C, 
   BF_REQUIRE((reinterpret_cast<uintptr_t>(in) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
              "bf_reorder: buffers must be 16-byte aligned");
   // Largest power-of-two time chunk (>= 8, dividing T) whose LDS image fits 64 KiB.
+  const char* ttc = bf::diag_env("BF_REORDER_TT");  // measurement: cap the time chunk
+  const int tt_cap = ttc ? atoi(ttc) : 1 << 30;
   int TT = 1;
-  while (TT * 2 <= T && T % (TT * 2) == 0) TT *= 2;
+  while (TT * 2 <= T && T % (TT * 2) == 0 && TT * 2 <= tt_cap) TT *= 2;
   while (TT > 8 && static_cast<long long>(A) * (TT * 4 + 4) > 65536) TT /= 2;
   BF_REQUIRE(static_cast<long long>(A) * (TT * 4 + 4) <= 65536, "bf_reorder: n_ants=%d too large", A);
   const int nchunk = T / TT;
@@ -138,12 +173,13 @@ extern "C" int bf_reorder(const uint8_t* in, uint8_t* out, int B, int A, int C, 
   const size_t lds = static_cast<size_t>(A) * (TT + 1) * 4;
   const char* e = bf::diag_env("BF_REORDER_ORDER");  // measurement: "channel" keeps the plain order
   const int xcd_range = grid % 8 == 0 && !(e && e[0] == 'c');
-  if (A % 8 == 0) {
-    hipLaunchKernelGGL(bf::reorder_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(256), lds,
-                       bf::as_stream(stream), in, out, A, C, T, TT, nchunk, xcd_range);
-  } else {
-    hipLaunchKernelGGL(bf::reorder_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(256), lds,
-                       bf::as_stream(stream), in, out, A, C, T, TT, nchunk, xcd_range);
-  }
+  const char* nt = bf::diag_env("BF_REORDER_NT");  // measurement: cache policy bits (1 loads, 2 stores)
+  const int cache = nt ? atoi(nt) : kReorderCache;
+  if (A % 8 == 0)
+    bf::launch_reorder<true>(cache, dim3(static_cast<unsigned>(grid)), lds, bf::as_stream(stream), in, out, A, C, T,
+                             TT, nchunk, xcd_range);
+  else
+    bf::launch_reorder<false>(cache, dim3(static_cast<unsigned>(grid)), lds, bf::as_stream(stream), in, out, A, C, T,
+                              TT, nchunk, xcd_range);
   BF_LAUNCHED("reorder_kernel");
 }

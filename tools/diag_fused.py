@@ -147,11 +147,13 @@ if _os.environ.get("I8_AB"):  # interleaved A/B: int8 item kernel with uniform-b
     for form, ts in ab.items():
         ts = sorted(ts)
         print(f"  i8 full, {form:8s} addressing  median {ts[len(ts) // 2] * 1e6:8.1f} us  min {ts[0] * 1e6:8.1f} us")
-for kbase, kname in ((32, "item"), (512, "i8")):
+names_f8 = {0: "full (f32 contract)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 5: "no-coef,no-store", 8: "no-load",
+            128: "cached loads", 64: "occ 4 bound", 96: "occ 3 bound"}
+for kbase, kname in ((32, "item"), (512, "i8"), (8192, "f8")):
     if _os.environ.get("DIAG_KERNELS", "item,i8").find(kname) < 0:
         continue
     only = _os.environ.get("DIAG_MODES")
-    modes = list(names_i8 if kname == "i8" else names)
+    modes = list(names_i8 if kname == "i8" else names_f8 if kname == "f8" else names)
     if only:
         modes = [m for m in modes if str(m) in only.split(",")]
     res = {m: [] for m in modes}
@@ -163,7 +165,8 @@ for kbase, kname in ((32, "item"), (512, "i8")):
     for mode in modes:
         ts = sorted(res[mode])
         med, mn = ts[len(ts) // 2], ts[0]
-        nm, ab = (names_i8[mode], alg_i8) if kname == "i8" else (names[mode], alg)
+        nm, ab = ((names_i8[mode], alg_i8) if kname == "i8" else (names_f8[mode], alg_i8) if kname == "f8"
+                  else (names[mode], alg))
         print(f"  {kname} mode {mode:3d} {nm:18s} median {med*1e6:8.1f} us  min {mn*1e6:8.1f} us  "
               f"alg {ab/med/1e9:7.1f} GB/s  ({len(ts)} rounds)")
 if _os.environ.get("DIAG_MIX"):  # the int8 path's 4:1 read:write mix, uniformly interleaved
@@ -199,7 +202,10 @@ if "table" in _os.environ.get("DIAG_KERNELS", ""):  # the MatrixMultiply drop-in
     yt = accel.DeviceArray(ctx, (B * 2 * C * T * 2 * M,), np.float32)
     _lib.call("bf_memset", wt.ptr, 0, wt.nbytes if hasattr(wt, "nbytes") else B * 2 * C * 2 * A * 2 * M * 4, q.handle)
     tb = 2 * B * 2 * C * T * A + B * 2 * C * 2 * A * 2 * M * 4 + B * 2 * C * T * 2 * M * 4
-    tnames.update({100: "8-byte loads (full)", 108: "8-byte loads, no x loads"})
+    tnames.update({100: "8-byte loads (full)", 108: "8-byte loads, no x loads", 200: "persistent (product)",
+                   201: "persistent, no LDS staging", 204: "persistent, no stores", 208: "persistent, no x loads",
+                   216: "persistent, no table loads", 217: "persistent, no table at all",
+                   220: "persistent, no table loads/stores", 228: "persistent, only MFMA+staging"})
     if _os.environ.get("TABLE_MODES"):  # e.g. 0,100: interleaved A/B over DIAG_ROUNDS, medians
         tnames = {int(m): tnames.get(int(m), str(m)) for m in _os.environ["TABLE_MODES"].split(",")}
     for nts in [int(v) for v in _os.environ.get("TABLE_NTS", "2,4").split(",")]:

@@ -24,8 +24,9 @@ for i, p in enumerate(PASSES):
     d = os.path.join(out, f"pass{i}")
     cmd = ["/opt/rocm/bin/rocprofv3", "--pmc", *p.split(), "--output-format", "csv", "-d", d, "-o", "pmc", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-pmc", "--no-secondary",
+           "--no-rocprof", "--no-ceiling",
            "--steps", "5", "--warmup", "2", *extra]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=ROOT, env=env)
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if r.returncode != 0 or not files:
         print(f"pass {i} failed rc={r.returncode}: {r.stderr[-400:]}")
