@@ -28,6 +28,7 @@
 //                             the delay model.  One workgroup per (b, c[, slab]), both pols.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "bf_mfma.hpp"
 
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
 // between the workgroup's start and its first MFMA.  The ring's last turn of an item prefetches the next item's
 // first steps.  Per item: convert the registers into the LDS slab, barrier, request the next slab, contract, barrier.
 // The MFMA sequence per output is the ring kernel's (bitwise the same results).
-template <bool Signed, int NTS, int R, int UPT, int Mode = 0>
+template <bool Signed, int NTS, int R, int UPT, int Mode = 0, int G = 2>
 __global__ __launch_bounds__(kThreads, 2) void beamform_table_persist_kernel(
     const uint8_t* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int NB, int A, int M, int S,
     int NT, int nslabs, long long nbpc, int xcd, long long nitems) {
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(kThreads, 2) void beamform_table_persist_kernel(
   const int K2 = 2 * A, M2 = 2 * M;
   const int Sp = (S + R - 1) / R * R;
   const int T = NB * kSamplesPerBlock;
-  constexpr int G = 2, R16 = R / 2, cols = NTS * 16;
+  constexpr int R16 = R / 2, cols = NTS * 16;
   const long long stride = gridDim.x;  // a multiple of 8: an item's XCD is its workgroup's
   // item -> (slab, bpc), the table_coords mapping; padding items (xcd groups past nbpc) are skipped
   auto coords = [&](long long it, int& slab, size_t& bpc) -> bool {
@@ -526,6 +527,172 @@ __global__ __launch_bounds__(kThreads, 2) void beamform_table_persist_kernel(
   }
 }
 
+// Output-stationary form for config 4's item shape (2M = 128 output columns, T = 256 samples, A % 64 == 0): one
+// workgroup of NW waves per (b, p, c) item holds the whole Y[256 x 128] in accumulators (wave w: 16 RG rows, RG =
+// 16 / NW row groups, all 8 column tiles) and streams K = 2A through LDS in chunks of 64 rows (two k-steps): the
+// chunk's table rows are read as whole 512-byte rows (thread = 8 rows x 16 / NW columns, converted to one hi and one
+// lo fragment per column), double-buffered, and each coefficient fragment feeds RG row groups x 2 MFMAs.  Against
+// the 32-column slab kernels this reads every item's voltages once instead of once per slab (4x at config 4) and the
+// table in whole rows instead of 128-byte row pieces.  Per output the MFMA sequence is the slab kernels' (k-steps in
+// order, hi then lo): bitwise the same sums.  NW = 8: 2 row groups per wave, 128 VGPRs, two workgroups (16 waves)
+// per CU; NW = 4: 4 row groups, 256 VGPRs, two workgroups (8 waves).  Mode (diagnostics): 4 no stores, 8 no voltage
+// loads, 16 no table loads.
+constexpr int kOsCols = 128, kOsRows = 256;
+constexpr size_t kOsLds = 2 * 2 * 8 * 2 * 64 * 16;  // 2 buffers x 2 steps x 8 tiles x 2 limbs x 64 lanes x 16 B
+
+template <bool Signed, int Mode, int NW>
+__global__ __launch_bounds__(NW * 64, NW / 2) void beamform_table_os_kernel(const uint8_t* __restrict__ x,
+                                                                      const float* __restrict__ w,
+                                                                      float* __restrict__ y, int A) {
+  extern __shared__ __attribute__((aligned(16))) half8 lds[];
+  constexpr int NTL = kOsCols / 16, RG = 16 / NW, M2 = kOsCols, T = kOsRows;
+  constexpr int CPT = 16 / NW;            // table columns per thread
+  constexpr int UPR = kOsCols / CPT;      // threads per row octet
+  constexpr int kBuf = 2 * NTL * 2 * 64;  // half8 per buffer
+  typedef float fvec __attribute__((ext_vector_type(CPT)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const size_t bpc = blockIdx.x;
+  const int K2 = 2 * A, nk = K2 / 64;  // chunks (even: A % 64 == 0)
+  const uint8_t* xp = x + bpc * static_cast<size_t>(T) * K2;
+  const float* wp = w + bpc * static_cast<size_t>(K2) * M2;
+  float* yp = y + bpc * static_cast<size_t>(T) * M2;
+
+  const int ro = tid / UPR, cq = tid % UPR;  // rows 8 ro .. 8 ro + 7 of a chunk x columns CPT cq ..
+  fvec tv[8];
+  auto tload = [&](int kc) __attribute__((always_inline)) {
+    if constexpr (Mode & 16) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) tv[j][i] = 1e-3f * (j + i) + 3e-3f * kc;
+      return;
+    }
+    // a uniform base + one 32-bit lane offset (the item's table is 2A x 128 floats)
+    const uint32_t off = static_cast<uint32_t>(((kc * 64 + 8 * ro) * M2 + CPT * cq) * 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      tv[j] = *reinterpret_cast<const fvec*>(reinterpret_cast<const char*>(wp) + off + j * M2 * 4);
+  };
+  auto tstore = [&](int buf) __attribute__((always_inline)) {
+    half8* L = lds + buf * kBuf;
+    const int sl = ro >> 2, hh = ro & 3;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int col = CPT * cq + i;
+      half8 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float wv = tv[j][i];
+        hi[j] = static_cast<_Float16>(wv);
+        lo[j] = static_cast<_Float16>(wv - static_cast<float>(hi[j]));  // exact difference, then rounded
+      }
+      const int slot = ((sl * NTL + (col >> 4)) * 2) * 64 + (col & 15) + 16 * hh;
+      L[slot] = hi;
+      L[slot + 64] = lo;
+    }
+  };
+  // voltages: row group rg of this wave = rows (RG wave + rg) 16 + tl; one 16-byte load = both k-steps of a chunk
+  const uint32_t xoff = static_cast<uint32_t>((RG * wave * 16 + tl) * K2 + 16 * h);  // lane offset in the item
+  auto xload = [&](int kc, uint4 (&xr)[RG]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+      if constexpr (Mode & 8)
+        xr[rg] = uint4{static_cast<uint32_t>(kc + tl), static_cast<uint32_t>(rg), static_cast<uint32_t>(kc - tl), 7u};
+      else
+        xr[rg] = *reinterpret_cast<const uint4*>(xp + (xoff + static_cast<uint32_t>(rg * 16 * K2 + 64 * kc)));
+    }
+  };
+  f32x4 acc[RG][NTL];
+#pragma unroll
+  for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) acc[rg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // contract the chunk in LDS buffer `buf` from the voltages in xr, then (next >= 0) reload xr with chunk `next`:
+  // the registers are free once re-dealt, so one voltage buffer keeps a chunk in flight
+  auto contract = [&](int buf, uint4 (&xr)[RG], int next) __attribute__((always_inline)) {
+    const half8* L = lds + buf * kBuf;
+    half8 v[RG];
+    uint32_t r1[RG][2];  // step 1's re-dealt dwords, converted after step 0
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {  // the ring kernel's re-deal: both steps' 8-byte fragments from one load
+      auto x0 = __builtin_amdgcn_permlane16_swap(xr[rg].x, xr[rg].z, false, false);
+      auto x1 = __builtin_amdgcn_permlane16_swap(xr[rg].y, xr[rg].w, false, false);
+      auto y0 = __builtin_amdgcn_permlane32_swap(x0[0], x0[1], false, false);
+      auto y1 = __builtin_amdgcn_permlane32_swap(x1[0], x1[1], false, false);
+      v[rg] = bytes8_to_frag<Signed>(y0[0], y1[0]);
+      r1[rg][0] = y0[1];
+      r1[rg][1] = y1[1];
+    }
+    if (next >= 0) xload(next, xr);  // uniform
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      if (sl == 1) {
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) v[rg] = bytes8_to_frag<Signed>(r1[rg][0], r1[rg][1]);
+      }
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) {
+        const int slot = ((sl * NTL + t) * 2) * 64 + lane;
+        const half8 chi = L[slot], clo = L[slot + 64];
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) {
+          acc[rg][t] = mfma(chi, v[rg], acc[rg][t]);
+          acc[rg][t] = mfma(clo, v[rg], acc[rg][t]);
+        }
+      }
+    }
+  };
+
+  uint4 xr[RG];
+  tload(0);
+  xload(0, xr);
+  tstore(0);
+  __syncthreads();
+  // chunk pairs: kc in LDS buffer 0, kc + 1 in buffer 1; each chunk's successor table is requested before the chunk
+  // is contracted (its voltages right after the re-deal: vmcnt is in order, so the table conversion waits for the
+  // table only).  The last pair requests nothing past the item (peeled, no clamped re-read).
+  auto pair = [&](int kc, auto more) __attribute__((always_inline)) {
+    tload(kc + 1);
+    contract(0, xr, kc + 1);
+    tstore(1);
+    __syncthreads();
+    if constexpr (decltype(more)::value) tload(kc + 2);
+    contract(1, xr, decltype(more)::value ? kc + 2 : -1);
+    if constexpr (decltype(more)::value) tstore(0);
+    __syncthreads();
+  };
+  for (int kc = 0; kc + 2 < nk; kc += 2) pair(kc, std::true_type{});
+  pair(nk - 2, std::false_type{});
+
+#pragma unroll
+  for (int rg = 0; rg < RG; ++rg) {
+    float* orow = yp + static_cast<size_t>((RG * wave + rg) * 16 + tl) * M2 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) {
+      if constexpr (Mode & 4) {
+        if (acc[rg][t][0] == 1234.5f) orow[t] = acc[rg][t][1];
+      } else {
+        *reinterpret_cast<f32x4*>(orow + 16 * t) = acc[rg][t];
+      }
+    }
+  }
+}
+
+// The output-stationary kernel's shape conditions (the caller's buffers: 16-byte aligned x and w rows).
+inline bool table_os_fits(int NB, int A, int M, const uint8_t* x, const float* w) {
+  return 2 * M == kOsCols && NB * kSamplesPerBlock == kOsRows && A % 64 == 0 && A >= 64 &&
+         (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0;
+}
+
+template <bool Signed, int Mode = 0, int NW = 8>
+int launch_table_os(const uint8_t* x, const float* w, float* y, long long bpc, int A, hipStream_t st) {
+  BF_REQUIRE(bpc < (1LL << 31), "bf_beamform: grid too large");
+  hipLaunchKernelGGL((beamform_table_os_kernel<Signed, Mode, NW>), dim3(static_cast<unsigned>(bpc)), dim3(NW * 64),
+                     kOsLds, st, x, w, y, A);
+  BF_LAUNCHED("beamform_table_os_kernel");
+}
+
 template <bool Signed, int NTS, bool Vec8>
 int launch_table(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                  hipStream_t st) {
@@ -562,7 +729,7 @@ int launch_ring(const uint8_t* x, const float* w, float* y, long long bpc, int N
 }
 
 // The persistent ring kernel: UPT table units per thread (Sp * NTS / 4 == UPT), two workgroups per CU.
-template <bool Signed, int NTS, int R, int UPT, int Mode = 0>
+template <bool Signed, int NTS, int R, int UPT, int Mode = 0, int G = 2>
 int launch_persist(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                    hipStream_t st) {
   const int nslabs = (NT + NTS - 1) / NTS;
@@ -577,7 +744,7 @@ int launch_persist(const uint8_t* x, const float* w, float* y, long long bpc, in
   const int n_cu = cu_count();
   const long long grid = std::min<long long>(nitems, xcd ? 2LL * n_cu / 8 * 8 : 2LL * n_cu);
   BF_REQUIRE(grid > 0 && (!xcd || grid % 8 == 0), "bf_beamform: persistent grid");
-  hipLaunchKernelGGL((beamform_table_persist_kernel<Signed, NTS, R, UPT, Mode>), dim3(static_cast<unsigned>(grid)),
+  hipLaunchKernelGGL((beamform_table_persist_kernel<Signed, NTS, R, UPT, Mode, G>), dim3(static_cast<unsigned>(grid)),
                      dim3(kThreads), lds, st, x, w, y, NB, A, M, S, NT, nslabs, bpc, xcd, nitems);
   BF_LAUNCHED("beamform_table_persist_kernel");
 }
@@ -611,6 +778,8 @@ int dispatch_vec(const uint8_t* x, const float* w, float* y, long long bpc, int 
 template <bool Signed>
 int dispatch_table(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                    hipStream_t st) {
+  const char* os = diag_env("BF_TABLE_OS");  // measurement: 0 keeps the slab kernels
+  if (table_os_fits(NB, A, M, x, w) && !(os && os[0] == '0')) return launch_table_os<Signed>(x, w, y, bpc, A, st);
   // Long rows (>= 16 k-steps: 256+ antennas): the widest slab whose staged fragments leave room for a second
   // workgroup per CU, so one workgroup's table staging overlaps the other's contraction (cfg4: a 128 KiB slab held
   // one workgroup per CU and ran 3.1 ms); the slabs' re-reads of x hit L2 (XCD-grouped slabs).
@@ -677,6 +846,19 @@ extern "C" int bf_diag_table(int mode, int nts, const uint8_t* x, const float* w
     case 217: return bf::launch_persist<true, 2, 16, 8, 17>(x, w, y, bpc, NB, A, M, S, NT, st);
     case 220: return bf::launch_persist<true, 2, 16, 8, 20>(x, w, y, bpc, NB, A, M, S, NT, st);
     case 228: return bf::launch_persist<true, 2, 16, 8, 28>(x, w, y, bpc, NB, A, M, S, NT, st);
+    // the output-stationary kernel (+ Mode bits)
+    case 400: return bf::launch_table_os<true, 0, 8>(x, w, y, bpc, A, st);
+    case 404: return bf::launch_table_os<true, 4, 8>(x, w, y, bpc, A, st);
+    case 408: return bf::launch_table_os<true, 8, 8>(x, w, y, bpc, A, st);
+    case 416: return bf::launch_table_os<true, 16, 8>(x, w, y, bpc, A, st);
+    case 428: return bf::launch_table_os<true, 28, 8>(x, w, y, bpc, A, st);
+    case 500: return bf::launch_table_os<true, 0, 4>(x, w, y, bpc, A, st);
+    case 528: return bf::launch_table_os<true, 28, 4>(x, w, y, bpc, A, st);
+    // four row groups per pass (each LDS coefficient fragment feeds 8 MFMAs instead of 4), ring depth 8
+    case 240: return bf::launch_persist<true, 2, 8, 8, 0, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 268: return bf::launch_persist<true, 2, 8, 8, 28, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 250: return bf::launch_persist<true, 2, 16, 8, 0, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
+    case 278: return bf::launch_persist<true, 2, 16, 8, 28, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
     case 300:  // the non-persistent 16-byte ring
       return nts == 4 ? bf::launch_ring<true, 4, 16>(x, w, y, bpc, NB, A, M, S, NT, st)
                       : bf::launch_ring<true, 2, 16>(x, w, y, bpc, NB, A, M, S, NT, st);

@@ -12,6 +12,9 @@
 // the 2M-wide output.
 #include <hip/hip_fp16.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "bf_common.hpp"
 #include "bf_phase.hpp"
 
@@ -100,8 +103,8 @@ __host__ __device__ inline int coef_block_ants(int A, int M) {
 
 template <int Cache>
 __global__ __launch_bounds__(256) void coeff_gen_block_kernel(const float4* __restrict__ dv, float* __restrict__ out,
-                                                              int BP, int C, int A, int M, int na, long long base_ch,
-                                                              double ctot, double ts) {
+                                                              int BP, int C, int A, int M, int na, int bpg,
+                                                              long long base_ch, double ctot, double ts) {
   extern __shared__ __attribute__((aligned(16))) float4 img4[];  // [antenna][M + 1] float4 (rows 2a, 2a + 1 + pad)
   float* img = reinterpret_cast<float*>(img4);
   const int c = static_cast<int>(blockIdx.y);
@@ -126,7 +129,8 @@ __global__ __launch_bounds__(256) void coeff_gen_block_kernel(const float4* __re
   for (int j = static_cast<int>(threadIdx.x); j < nb * M; j += 256) {  // 16-byte pieces of the run
     const int la = j / M;
     const float4 v = img4[la * (M + 1) + (j - la * M)];
-    for (int bp = 0; bp < BP; ++bp) {
+    const int bp1 = min(BP, (static_cast<int>(blockIdx.z) + 1) * bpg);
+    for (int bp = static_cast<int>(blockIdx.z) * bpg; bp < bp1; ++bp) {
       float4* o = dst + static_cast<size_t>(bp) * (bp_stride >> 2) + j;
       if constexpr (Cache & 2) {
         typedef float f4v __attribute__((ext_vector_type(4)));
@@ -187,15 +191,20 @@ extern "C" int bf_coeff_gen(const float* delay_vals, float* out, int B, int P, i
     const unsigned gx = static_cast<unsigned>((A + na - 1) / na);
     const size_t lds = static_cast<size_t>(na) * (M + 1) * 16;
     const char* nt = bf::diag_env("BF_COEFF_NT");
+    const char* bg = bf::diag_env("BF_COEFF_BPG");  // measurement: (b, p) planes per workgroup
+    // up to 4 (b, p) planes per workgroup: cfg3 (16 planes) 245 -> 189 us, non-temporal (plain 245 us); one plane
+    // per workgroup recomputes the phasors too often (300 us) -- profiles/r3_k_ops_ab.txt
+    const int bpg = bg ? std::max(1, atoi(bg)) : std::min(B * P, 4);
+    const unsigned gz = static_cast<unsigned>((B * P + bpg - 1) / bpg);
     const auto dv = reinterpret_cast<const float4*>(delay_vals);
     const long long base = static_cast<long long>(C) * xeng_id;
     if (nt && nt[0] == '0')
-      hipLaunchKernelGGL(bf::coeff_gen_block_kernel<0>, dim3(gx, static_cast<unsigned>(C)), dim3(256), lds,
-                         bf::as_stream(stream), dv, out, B * P, C, A, M, na, base, static_cast<double>(Ctot),
+      hipLaunchKernelGGL(bf::coeff_gen_block_kernel<0>, dim3(gx, static_cast<unsigned>(C), gz), dim3(256), lds,
+                         bf::as_stream(stream), dv, out, B * P, C, A, M, na, bpg, base, static_cast<double>(Ctot),
                          sample_period);
     else
-      hipLaunchKernelGGL(bf::coeff_gen_block_kernel<2>, dim3(gx, static_cast<unsigned>(C)), dim3(256), lds,
-                         bf::as_stream(stream), dv, out, B * P, C, A, M, na, base, static_cast<double>(Ctot),
+      hipLaunchKernelGGL(bf::coeff_gen_block_kernel<2>, dim3(gx, static_cast<unsigned>(C), gz), dim3(256), lds,
+                         bf::as_stream(stream), dv, out, B * P, C, A, M, na, bpg, base, static_cast<double>(Ctot),
                          sample_period);
     BF_LAUNCHED("coeff_gen_block_kernel");
   }

@@ -154,10 +154,8 @@ __device__ __forceinline__ void make_coefs(_Float16* lh, const CoefPrefetch<NTS>
       if (P.gain) apply_gain(cp.g[j], &re, &im);
     }
     const int cl = 2 * ml;
-    put_split(lh, coef_elem(2 * a, cl, nts), re);          // W[2a][2m]     =  cos
-    put_split(lh, coef_elem(2 * a, cl + 1, nts), im);      // W[2a][2m+1]   =  sin
-    put_split(lh, coef_elem(2 * a + 1, cl, nts), -im);     // W[2a+1][2m]   = -sin
-    put_split(lh, coef_elem(2 * a + 1, cl + 1, nts), re);  // W[2a+1][2m+1] =  cos
+    put_split2(lh, coef_elem(2 * a, cl, nts), re, -im);     // W[2a][2m] = cos, W[2a+1][2m] = -sin
+    put_split2(lh, coef_elem(2 * a, cl + 1, nts), im, re);  // W[2a][2m+1] = sin, W[2a+1][2m+1] = cos
   }
 }
 
@@ -185,10 +183,8 @@ __device__ __forceinline__ void gen_coefs(_Float16* lh, const FusedArgs& P, int 
       if (P.gain) apply_gain(P.gain[m * P.A + a], &re, &im);
     }
     const int cl = 2 * ml;
-    put_split(lh, coef_elem(2 * a, cl, nts), re);
-    put_split(lh, coef_elem(2 * a, cl + 1, nts), im);
-    put_split(lh, coef_elem(2 * a + 1, cl, nts), -im);
-    put_split(lh, coef_elem(2 * a + 1, cl + 1, nts), re);
+    put_split2(lh, coef_elem(2 * a, cl, nts), re, -im);
+    put_split2(lh, coef_elem(2 * a, cl + 1, nts), im, re);
   }
 }
 

@@ -61,6 +61,17 @@ __device__ __forceinline__ void put_split(_Float16* lh, int e, float w) {
   lh[e + 64 * 8] = lo;  // the lo fragment follows the hi fragment (next 1 KiB)
 }
 
+// Rows k = 2a and 2a + 1 of one column are adjacent halves of a lane's fragment (coef_elem(2a + 1, cl) =
+// coef_elem(2a, cl) + 1): one 4-byte LDS write per limb for the pair instead of two 2-byte writes.
+__device__ __forceinline__ void put_split2(_Float16* lh, int e, float w0, float w1) {
+  const _Float16 h0 = static_cast<_Float16>(w0), h1 = static_cast<_Float16>(w1);
+  const _Float16 l0 = static_cast<_Float16>(w0 - static_cast<float>(h0));
+  const _Float16 l1 = static_cast<_Float16>(w1 - static_cast<float>(h1));
+  typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+  *reinterpret_cast<h2v*>(lh + e) = h2v{h0, h1};
+  *reinterpret_cast<h2v*>(lh + e + 64 * 8) = h2v{l0, l1};
+}
+
 template <int NTS>
 __device__ __forceinline__ void store_f32(float* orow, int col0, int M2, const f32x4& v) {
   if ((M2 & 3) == 0 && col0 + 4 <= M2) {

@@ -150,7 +150,9 @@ void launch_reorder(int cache, dim3 grid, size_t lds, hipStream_t st, const uint
 }  // namespace bf
 
 namespace {
-constexpr int kReorderCache = 0;  // the product's cache policy (see launch_reorder)
+// the product's cache policy: non-temporal loads and stores (cfg3 831 -> 723 us, cfg4 447 -> 413 us;
+// profiles/r3_j_ops_ab.txt)
+constexpr int kReorderCache = 3;
 }
 
 extern "C" int bf_reorder(const uint8_t* in, uint8_t* out, int B, int A, int C, int T, void* stream) {

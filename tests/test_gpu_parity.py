@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from dpdk_dc_sand_amd import _lib
+from dpdk_dc_sand_amd import _lib, accel
 from dpdk_dc_sand_amd.beamforming import (CoeffGeneratorTemplate, FusedBeamformerTemplate, MatrixMultiplyTemplate,
                                           OpSequenceTemplate, PreBeamformReorderTemplate, RequantTemplate)
 from golden_io import cases, get, voltages
@@ -224,13 +224,14 @@ def test_matrix_multiply_random_tables(context, command_queue, A, M, C, T, signe
     assert_beams_allclose(y, O.complex_mult(x, w, signed=signed), x, w, signed=signed)
 
 
-@pytest.mark.parametrize("T,signed", [(32, True), (256, False)])
+@pytest.mark.parametrize("T,signed", [(32, True), (128, False)])
 def test_matrix_multiply_persistent_equals_ring(context, command_queue, T, signed):
     """256 antennas in two-workgroup slabs with >= 8 (b, p, c) items take the persistent table kernel (the next
     slab loaded under the current item, the ring's last turn prefetching the next item's rows; 640 slab items here,
     more than one per workgroup, xcd padding items skipped).  Its per-item MFMA sequence is the ring kernel's, which
     one-channel calls (4 items) still take: the results must be identical bits, and within tolerance of the oracle.
-    T = 32 leaves two of the four waves without row groups; T = 256 gives each wave two row-group pairs."""
+    T = 32 leaves two of the four waves without row groups; T = 128 gives each wave one row-group pair (T = 256
+    takes the output-stationary kernel, tested below)."""
     B, A, M, C = 2, 256, 64, 40
     rng = np.random.default_rng(T + 5)
     x = rng.integers(0, 256, (B, 2, C, T // 16, 16, A, 2), dtype=np.uint8)
@@ -261,6 +262,32 @@ def test_matrix_multiply_persistent_single_slab_any_item_count(context, command_
     op = MatrixMultiplyTemplate(context, A, C, T, M, B).instantiate(command_queue)
     (y,) = run(op, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
     assert_beams_allclose(y, O.complex_mult(x, w), x, w)
+
+
+@pytest.mark.parametrize("A,C,signed", [(256, 6, False), (256, 3, True), (128, 4, False), (64, 5, True)])
+def test_matrix_multiply_output_stationary_equals_slab_kernels(context, command_queue, A, C, signed):
+    """Config 4's item shape (2M = 128 columns, T = 256, A % 64 == 0) takes the output-stationary table kernel
+    (whole items per workgroup, K streamed through LDS).  A table pointer that is only 4-byte aligned keeps the
+    same call on the slab kernels (ring / persistent): per output both run the same MFMA sequence, so the bits
+    must be equal -- and within tolerance of the oracle."""
+    B, M, T = 2, 64, 256
+    rng = np.random.default_rng(A + C)
+    x = rng.integers(0, 256, (B, 2, C, T // 16, 16, A, 2), dtype=np.uint8)
+    if signed:
+        x = x.view(np.int8)
+    w = rng.uniform(-1.0, 1.0, (B, 2, C, 2 * A, 2 * M)).astype(np.float32)
+    op = MatrixMultiplyTemplate(context, A, C, T, M, B, sample_signed=signed).instantiate(command_queue)
+    (y,) = run(op, command_queue, {"inData": x, "inCoeffs": w}, ["outData"])
+    xd = accel.DeviceArray(context, x.shape, x.dtype)
+    xd.set(command_queue, x)
+    wd = accel.DeviceArray(context, (w.size + 4,), np.float32)
+    wd.set(command_queue, np.concatenate([np.zeros(1, np.float32), w.reshape(-1), np.zeros(3, np.float32)]))
+    yd = accel.DeviceArray(context, y.shape, np.float32)
+    _lib.call("bf_beamform", xd.ptr, wd.ptr + 4, yd.ptr, B, 2, C, T // 16, A, M, int(signed), command_queue.handle)
+    np.testing.assert_array_equal(y, yd.get(command_queue))
+    sel = [0, C - 1]
+    xs, ws = np.ascontiguousarray(x[:, :, sel]), np.ascontiguousarray(w[:, :, sel])
+    assert_beams_allclose(y[:, :, sel], O.complex_mult(xs, ws, signed=signed), xs, ws, signed=signed)
 
 
 # ---- full sequence (beamform_op_sequence_test.py:37-200) ---------------------------------------------------

@@ -205,7 +205,11 @@ if "table" in _os.environ.get("DIAG_KERNELS", ""):  # the MatrixMultiply drop-in
     tnames.update({100: "8-byte loads (full)", 108: "8-byte loads, no x loads", 200: "persistent (product)",
                    201: "persistent, no LDS staging", 204: "persistent, no stores", 208: "persistent, no x loads",
                    216: "persistent, no table loads", 217: "persistent, no table at all",
-                   220: "persistent, no table loads/stores", 228: "persistent, only MFMA+staging"})
+                   220: "persistent, no table loads/stores", 228: "persistent, only MFMA+staging",
+                   240: "persistent G4 R8", 268: "persistent G4 R8, only MFMA+staging", 250: "persistent G4 R16",
+                   278: "persistent G4 R16, only MFMA+staging", 400: "output-stationary", 404: "os, no stores",
+                   408: "os, no x loads", 416: "os, no table loads", 428: "os, only MFMA+staging",
+                   500: "os 4 waves", 528: "os 4 waves, only MFMA+staging"})
     if _os.environ.get("TABLE_MODES"):  # e.g. 0,100: interleaved A/B over DIAG_ROUNDS, medians
         tnames = {int(m): tnames.get(int(m), str(m)) for m in _os.environ["TABLE_MODES"].split(",")}
     for nts in [int(v) for v in _os.environ.get("TABLE_NTS", "2,4").split(",")]:

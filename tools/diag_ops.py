@@ -67,7 +67,8 @@ def main():
         raw.set(q, rng.integers(0, 256, vb, dtype=np.uint8))
         ro = accel.DeviceArray(ctx, (vb,), np.uint8)
         reorder = {f"nt{nt} tt{tt}": {"BF_REORDER_NT": str(nt), "BF_REORDER_TT": str(tt)}
-                   for nt in (0, 1, 2, 3) for tt in (32, 64, 128, 256)}
+                   for nt in [int(v) for v in os.environ.get("REORDER_NT", "0,1,2,3").split(",")]
+                   for tt in [int(v) for v in os.environ.get("REORDER_TT", "32,64,128,256").split(",")]}
         res = {k: [] for k in reorder}
         ref = None
         for k, env in reorder.items():  # equality first
@@ -94,6 +95,10 @@ def main():
         tb = B * 2 * C * 2 * A * 2 * M * 4
         out = accel.DeviceArray(ctx, (tb // 4,), np.float32)
         forms = {"block nt": {"BF_COEFF_NT": "1"}, "block plain": {"BF_COEFF_NT": "0"},
+                 "block nt bpg4": {"BF_COEFF_NT": "1", "BF_COEFF_BPG": "4"},
+                 "block plain bpg4": {"BF_COEFF_NT": "0", "BF_COEFF_BPG": "4"},
+                 "block nt bpg1": {"BF_COEFF_NT": "1", "BF_COEFF_BPG": "1"},
+                 "block plain bpg1": {"BF_COEFF_NT": "0", "BF_COEFF_BPG": "1"},
                  "per-(a,m) thread": {"BF_COEFF_FORM": "thread"}, "per-(a,m) tile": {"BF_COEFF_FORM": "tile"}}
         ref = None
         for k, env in forms.items():
