@@ -463,6 +463,13 @@ def rocprof_check(args, n_secondary):
     return regions, child, None
 
 
+def short_kernel(name):
+    """'void bf::(anonymous namespace)::k<true, 2>(bf::FusedArgs)' -> 'k<true, 2>'."""
+    name = name.replace("(anonymous namespace)::", "")
+    name = name[5:] if name.startswith("void ") else name
+    return name.split("(")[0].split("::")[-1][:70]
+
+
 def rocprof_entry(regions, i, kernel, alg_bytes):
     """The timed dispatches of `kernel` in region i: count, average / median duration, roofline fraction."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -480,7 +487,7 @@ def rocprof_entry(regions, i, kernel, alg_bytes):
            "frac": round(alg_bytes / (per_step_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)}
     if len(regions[i]) > 1:
         out["per_step_us_all_kernels"] = round(per_step_ns / 1e3, 2)
-        out["kernels_us_per_step"] = {k.split("(")[0].split("::")[-1][:60]: round(v["TotalDurationNs"] / steps / 1e3, 2)
+        out["kernels_us_per_step"] = {short_kernel(k): round(v["TotalDurationNs"] / steps / 1e3, 2)
                                       for k, v in regions[i].items()}
     return out
 

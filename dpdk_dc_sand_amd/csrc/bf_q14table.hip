@@ -23,6 +23,7 @@
 // slot-antenna group g of 8) and slot antenna i of the group -- one 16-byte load per lane per half unit there, and
 // 256 contiguous bytes per wave-store here.
 #include <algorithm>
+#include <cstdlib>
 
 #include "bf_fused.hpp"
 
@@ -36,7 +37,7 @@ struct Q14TableArgs {
   const float4* dv;
   const float* gain;
   uint32_t* out;
-  int delay_channels, B, C, A, M, Sp, nslabs, layout;
+  int delay_channels, B, C, A, M, Sp, nslabs, layout, run;
   long long base_ch;
   double ctot, ts, k, t0, batch_dt;
 };
@@ -52,7 +53,7 @@ __device__ __forceinline__ bool w32_slot_antenna(int sa, int A, int* a) {
 template <bool Gain>
 __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
   const int b = blockIdx.z;
-  const int c0 = blockIdx.y * kQ14Run;
+  const int c0 = blockIdx.y * P.run;
   const int w = blockIdx.x * 256 + threadIdx.x;  // word within a (b, c[, slab]) block
   int a, m, slab = 0;
   bool valid;
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
     words = static_cast<size_t>(per_slab) * P.nslabs;
     base = (static_cast<size_t>(b) * P.C + c0) * words + w;
   }
-  const int nrun = min(kQ14Run, P.C - c0);
+  const int nrun = min(P.run, P.C - c0);
   uint32_t* o = P.out + base;
   if (!valid) {
     for (int j = 0; j < nrun; ++j) o[static_cast<size_t>(j) * words] = 0u;
@@ -139,7 +140,11 @@ int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t 
   Q.ctot = P.ctot, Q.ts = P.ts, Q.k = P.k, Q.t0 = P.t0, Q.batch_dt = P.batch_dt;
   const long long words = layout == kLayoutNatural ? static_cast<long long>(P.M) * P.A
                                                    : 1024LL * Q.Sp * Q.nslabs;
-  const long long gx = (words + 255) / 256, gy = (P.C + kQ14Run - 1) / kQ14Run;
+  // measurement: channels per recurrence run (16 / 32 / 64 / 128 / 256: 97 / 88 / 78-80 / 78 / 81 us at config 4;
+  // four words per thread with 16-byte stores, plain or non-temporal: 87-90 us -- profiles/r3_o_generator_sweep.txt)
+  const char* rn = diag_env("BF_Q14_RUN");
+  Q.run = rn ? std::max(1, atoi(rn)) : kQ14Run;
+  const long long gx = (words + 255) / 256, gy = (P.C + Q.run - 1) / Q.run;
   BF_REQUIRE(gx < (1LL << 31) && gy < 65536 && P.B < 65536, "q14 table: grid too large");
   if (P.gain)
     hipLaunchKernelGGL(q14_table_kernel<true>, dim3(static_cast<unsigned>(gx), static_cast<unsigned>(gy), P.B),
