@@ -443,7 +443,7 @@ def rocprof_check(args, n_secondary):
         return None, None, "rocprofv3 not found"
     out = args.prof_out or tempfile.mkdtemp(prefix="bfprof_", dir=os.environ.get("TMPDIR", "/tmp"))
     os.makedirs(out, exist_ok=True)
-    cmd = [exe, "--kernel-trace", "--output-format", "csv", "-d", out, "-o", "bench", "--", sys.executable,
+    cmd = [exe, "--kernel-trace", "--stats", "--output-format", "csv", "-d", out, "-o", "bench", "--", sys.executable,
            os.path.abspath(__file__), "--prof-child", "--workload", args.workload, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--settle-ms", str(args.settle_ms), "--output", args.output,
            "--int8-contract", args.int8_contract, "--coeff-table", args.coeff_table, "--no-pmc", "--no-cpu-baseline",

@@ -1506,6 +1506,8 @@ extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void
       case 128: return bf::launch_item<true, true, 2, false, true, 128>(P, st);
       case 64: return bf::launch_item<true, true, 2, false, true, 0, 4>(P, st);
       case 96: return bf::launch_item<true, true, 2, false, true, 0, 3>(P, st);
+      case 16: return bf::launch_item<true, true, 2, true, true, 0, 4>(P, st);  // exact coefficients (product occ)
+      case 80: return bf::launch_item<true, true, 2, true, true, 0, 1>(P, st);  // exact, unbounded
       default: bf::set_error("bad mode"); return BF_ERR_ARG;
     }
   }

@@ -19,8 +19,9 @@ for s in $STAGES; do
     diag)   env ${DIAG_ENV} DIAG_STREAMS=${DIAG_STREAMS:-0} timeout -k 10 300 python tools/diag_fused.py ${DIAG_SHAPE:-1 4096 256 256 64} > $OUT/diag.txt 2>&1 || { echo "diag failed"; tail -20 $OUT/diag.txt; exit 1; }; cat $OUT/diag.txt ;;
     ops)    timeout -k 10 400 python tools/bench_ops.py ${OPS_ARGS} > $OUT/ops.jsonl 2> $OUT/ops.err || { echo "ops failed"; tail -20 $OUT/ops.err; exit 1; }; cat $OUT/ops.jsonl ;;
     pmc)    timeout -k 10 600 python tools/pmc_profile.py $OUT/pmc -- ${BENCH_ARGS} > $OUT/pmc.txt 2>&1 || { echo "pmc failed"; tail -20 $OUT/pmc.txt; exit 1; }; cat $OUT/pmc.txt ;;
+    stream) timeout -k 10 300 python tools/bench_stream.py > $OUT/stream.json 2> $OUT/stream.err || { echo "stream failed"; tail -20 $OUT/stream.err; exit 1; }; cat $OUT/stream.json ;;
     cal)    timeout -k 10 300 python tools/pmc_calibrate.py $OUT/cal > $OUT/pmc_calibration.jsonl 2>&1 || { echo "cal failed"; exit 1; }; cat $OUT/pmc_calibration.jsonl ;;
-    prof)   timeout -k 10 600 /opt/rocm/bin/rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --no-cpu-baseline --no-pmc --no-secondary --no-ceiling ${BENCH_ARGS} > $OUT/prof_bench.json 2> $OUT/prof.log || { echo "prof failed"; tail -20 $OUT/prof.log; exit 1; } ;;
+    prof)   timeout -k 10 600 /opt/rocm/bin/rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --no-cpu-baseline --no-pmc --no-secondary --no-ceiling --no-rocprof ${BENCH_ARGS} > $OUT/prof_bench.json 2> $OUT/prof.log || { echo "prof failed"; tail -20 $OUT/prof.log; exit 1; } ;;
   esac
   echo "stage $s ok"
 done
