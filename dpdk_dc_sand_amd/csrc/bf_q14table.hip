@@ -164,6 +164,7 @@ extern "C" int bf_q14_coeffs(const float* delay_vals, int delay_channels, const 
   BF_REQUIRE(B > 0 && C > 0 && A > 0 && M > 0 && Ctot > 0 && xeng_id >= 0,
              "bf_q14_coeffs: bad shape B=%d C=%d A=%d M=%d Ctot=%d", B, C, A, M, Ctot);
   BF_REQUIRE(delay_channels == 1 || delay_channels == C, "bf_q14_coeffs: delay_channels must be 1 or C");
+  BF_REQUIRE(static_cast<long long>(M) * A < (1LL << 31) && C < (1 << 30), "bf_q14_coeffs: shape too large");
   BF_REQUIRE(sample_period > 0.0, "bf_q14_coeffs: sample_period must be > 0");
   BF_REQUIRE((reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 3) == 0,
              "bf_q14_coeffs: misaligned buffer");
