@@ -96,7 +96,22 @@ struct bf_comm {
   size_t staging_bytes = 0;
   double* d_scalar = nullptr;  // allreduce scratch
   hipStream_t stream = nullptr;
+  hipEvent_t sent = nullptr;   // root: recorded after the last scatter's sends (the staging buffer's last reader)
 };
+
+namespace {
+// The communicator's device for the duration of a call (the caller's device restored on return).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+}  // namespace
 
 extern "C" {
 
@@ -124,7 +139,9 @@ int bf_comm_create(bf_comm** out, const void* id, size_t len, int nranks, int ra
   hipError_t e = hipGetDevice(&c->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_scalar), sizeof(double));
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sent, hipEventDisableTiming);
   if (e != hipSuccess) {
+    if (c->d_scalar) (void)hipFree(c->d_scalar);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return bf::hip_fail(e, "bf_comm_create");
@@ -134,6 +151,7 @@ int bf_comm_create(bf_comm** out, const void* id, size_t len, int nranks, int ra
   const ncclResult_t r = rccl().comm_init_rank(&c->comm, nranks, u, rank);
   if (r != ncclSuccess) {
     (void)hipFree(c->d_scalar);
+    (void)hipEventDestroy(c->sent);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return rccl_fail(r, "ncclCommInitRank");
@@ -150,8 +168,12 @@ int bf_comm_destroy(bf_comm* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   const ncclResult_t r = c->comm ? rccl().comm_destroy(c->comm) : ncclSuccess;
-  if (c->staging) (void)hipFree(c->staging);
+  if (c->staging) {
+    (void)hipEventSynchronize(c->sent);
+    (void)hipFree(c->staging);
+  }
   (void)hipFree(c->d_scalar);
+  (void)hipEventDestroy(c->sent);
   (void)hipStreamDestroy(c->stream);
   delete c;
   if (prev >= 0) (void)hipSetDevice(prev);
@@ -161,6 +183,7 @@ int bf_comm_destroy(bf_comm* c) {
 
 int bf_comm_allreduce_max(bf_comm* c, double* value) {
   BF_REQUIRE(c != nullptr && value != nullptr, "bf_comm_allreduce_max: null pointer");
+  DeviceGuard dg(c->device);
   BF_HIP(hipMemcpyAsync(c->d_scalar, value, sizeof(double), hipMemcpyHostToDevice, c->stream));
   BF_RCCL(rccl().all_reduce(c->d_scalar, c->d_scalar, 1, ncclFloat64, ncclMax, c->comm, c->stream));
   BF_HIP(hipMemcpyAsync(value, c->d_scalar, sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -174,6 +197,7 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
   BF_REQUIRE(B > 0 && A > 0 && C > 0 && T > 0, "bf_channel_scatter: bad shape B=%d A=%d C=%d T=%d", B, A, C, T);
   BF_REQUIRE(root >= 0 && root < c->nranks, "bf_channel_scatter: root %d of %d ranks", root, c->nranks);
   BF_REQUIRE(c->rank != root || band != nullptr, "bf_channel_scatter: the root needs the band");
+  DeviceGuard dg(c->device);
   hipStream_t st = bf::as_stream(stream);
   const size_t run = static_cast<size_t>(C) * T * 4;            // one (b, a) channel run of a slice
   const size_t pitch = run * static_cast<size_t>(c->nranks);    // the band's (b, a) row
@@ -183,7 +207,7 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
     const size_t need = slice_bytes * static_cast<size_t>(c->nranks - 1);
     if (need > c->staging_bytes) {
       if (c->staging) {
-        BF_HIP(hipStreamSynchronize(st));
+        BF_HIP(hipEventSynchronize(c->sent));
         BF_HIP(hipFree(c->staging));
         c->staging = nullptr;
         c->staging_bytes = 0;
@@ -191,6 +215,8 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
       BF_HIP(hipMalloc(&c->staging, need));
       c->staging_bytes = need;
     }
+    // the previous scatter's sends may still read the staging buffer on another stream
+    BF_HIP(hipStreamWaitEvent(st, c->sent, 0));
     uint8_t* stg = static_cast<uint8_t*>(c->staging);
     for (int r = 0, k = 0; r < c->nranks; ++r) {
       uint8_t* dst = r == root ? slice : stg + slice_bytes * static_cast<size_t>(k++);
@@ -209,6 +235,7 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
       }
     }
     BF_RCCL(rccl().group_end());
+    BF_HIP(hipEventRecord(c->sent, st));
   } else {
     BF_RCCL(rccl().recv(slice, slice_bytes, ncclUint8, root, c->comm, st));
   }
