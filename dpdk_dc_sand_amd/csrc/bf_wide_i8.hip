@@ -1121,7 +1121,8 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   case m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
   case 100 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
   case 300 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 400 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 4>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break
+  case 400 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 4>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, true, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break
   switch (mode) {
     BF_W32T(0); BF_W32T(1); BF_W32T(4); BF_W32T(8); BF_W32T(9); BF_W32T(12);
     default: return BF_ERR_ARG;

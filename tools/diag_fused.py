@@ -85,6 +85,7 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
     tnames.update({100 + m: v.replace("early", "late") + (" (late)" if m else "") for m, v in base.items()})
     tnames.update({300 + m: v.replace("early ", "") + " [unrolled NB3]" for m, v in base.items()})
     tnames.update({400 + m: v.replace("early ", "") + " [unrolled NB4]" for m, v in base.items()})
+    tnames.update({500 + m: v + " [unrolled NB3, early table]" for m, v in base.items()})
     if _os.environ.get("W32T_MODES"):
         tnames = {int(m): tnames.get(int(m), str(m)) for m in _os.environ["W32T_MODES"].split(",")}
     alg8 = nin + nout // 4
@@ -149,11 +150,13 @@ if _os.environ.get("I8_AB"):  # interleaved A/B: int8 item kernel with uniform-b
         print(f"  i8 full, {form:8s} addressing  median {ts[len(ts) // 2] * 1e6:8.1f} us  min {ts[0] * 1e6:8.1f} us")
 names_f8 = {0: "full (f32 contract)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 5: "no-coef,no-store", 8: "no-load",
             128: "cached loads", 64: "occ 4 bound", 96: "occ 3 bound", 16: "exact coef, occ 4", 80: "exact coef"}
-for kbase, kname in ((32, "item"), (512, "i8"), (8192, "f8")):
+names_fs = {0: "staged 1 KiB f32 stores", 4: "staged, no-store", 128: "staged, cached loads", 256: "staged, nt stores",
+            384: "staged, cached loads, nt st", 192: "staged, cached, occ 3"}
+for kbase, kname in ((32, "item"), (512, "i8"), (8192, "f8"), (16384, "fs")):
     if _os.environ.get("DIAG_KERNELS", "item,i8").find(kname) < 0:
         continue
     only = _os.environ.get("DIAG_MODES")
-    modes = list(names_i8 if kname == "i8" else names_f8 if kname == "f8" else names)
+    modes = list(names_i8 if kname == "i8" else names_f8 if kname == "f8" else names_fs if kname == "fs" else names)
     if only:
         modes = [m for m in modes if str(m) in only.split(",")]
     res = {m: [] for m in modes}
@@ -166,7 +169,7 @@ for kbase, kname in ((32, "item"), (512, "i8"), (8192, "f8")):
         ts = sorted(res[mode])
         med, mn = ts[len(ts) // 2], ts[0]
         nm, ab = ((names_i8[mode], alg_i8) if kname == "i8" else (names_f8[mode], alg_i8) if kname == "f8"
-                  else (names[mode], alg))
+                  else (names_fs[mode], alg) if kname == "fs" else (names[mode], alg))
         print(f"  {kname} mode {mode:3d} {nm:18s} median {med*1e6:8.1f} us  min {mn*1e6:8.1f} us  "
               f"alg {ab/med/1e9:7.1f} GB/s  ({len(ts)} rounds)")
 if _os.environ.get("DIAG_MIX"):  # the int8 path's 4:1 read:write mix, uniformly interleaved
