@@ -142,6 +142,18 @@ __device__ __forceinline__ int q14_pair(double v, float gq, bool* ok) {
   return static_cast<int>(qa);
 }
 
+// Unit gain: Q = rint(2^14 * RN32(v)).  The Q14 boundaries (2k + 1) / 2^15 are float32 numbers, so RN32 keeps v on
+// its side of every boundary unless v lies within half a float32 ulp (<= 2^-24 for |v| <= 1) of it: with t = 2^14 v,
+// Q = rint(t) whenever |t - rint(t)| < 1/2 - 2^14 (eps + 2^-24) (4 float64 operations).  Only the ~0.2 % of values
+// nearer a boundary take q14_pair's two-sided test (which still decides almost all of them: Q(RN32(v -+ eps)) agree).
+constexpr double kQ14UnitMargin = 0.5 - 16384.0 * (kQ14Eps + 0x1p-24);
+__device__ __forceinline__ int q14_pair_unit(double v, bool* ok) {
+  const double t = v * 16384.0;
+  const double n = rint(t);
+  if (fabs(t - n) < kQ14UnitMargin) return static_cast<int>(n);
+  return q14_pair(v, 16384.0f, ok);
+}
+
 // The truncated fdlibm coefficients (cos C5..C1, -1/2; sin S5..S1) as device memory, not literals: loaded once into
 // SGRPs by s_load, each Horner step is then one VOP3 v_fma_f64 with an SGPR operand, where literal constants made
 // the compiler rematerialise every addend with two v_mov_b32 per step (21 of ~96 VALU per phasor).

@@ -37,7 +37,7 @@ struct Q14TableArgs {
   const float4* dv;
   const float* gain;
   uint32_t* out;
-  int delay_channels, B, C, A, M, Sp, nslabs, layout, run;
+  int delay_channels, B, C, A, M, Sp, nslabs, layout, run, unit_fast;
   long long base_ch;
   double ctot, ts, k, t0, batch_dt;
 };
@@ -115,7 +115,14 @@ __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
   }
   for (int j = 0; j < nrun; ++j) {
     bool ok = in_range;
-    int wc = q14_pair(re, gq, &ok), ws = q14_pair(im, gq, &ok);
+    int wc, ws;
+    if (Gain || !P.unit_fast) {  // (uniform)
+      wc = q14_pair(re, gq, &ok);
+      ws = q14_pair(im, gq, &ok);
+    } else {
+      wc = q14_pair_unit(re, &ok);
+      ws = q14_pair_unit(im, &ok);
+    }
     if (!ok) q14_exact(d, static_cast<double>(P.base_ch + c0 + j), P.ctot, P.ts, dt, P.gain, g, &wc, &ws);
     o[static_cast<size_t>(j) * words] = (static_cast<uint32_t>(wc) & 0xffffu) | (static_cast<uint32_t>(ws) << 16);
     const double r2 = fma(re, cd, -im * sd);
@@ -144,6 +151,8 @@ int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t 
   // four words per thread with 16-byte stores, plain or non-temporal: 87-90 us -- profiles/r3_o_generator_sweep.txt)
   const char* rn = diag_env("BF_Q14_RUN");
   Q.run = rn ? std::max(1, atoi(rn)) : kQ14Run;
+  const char* uf = diag_env("BF_Q14_UNIT");  // measurement: 0 = the two-sided decision for unit gains too
+  Q.unit_fast = !(uf && uf[0] == '0');
   const long long gx = (words + 255) / 256, gy = (P.C + Q.run - 1) / Q.run;
   BF_REQUIRE(gx < (1LL << 31) && gy < 65536 && P.B < 65536, "q14 table: grid too large");
   if (P.gain)

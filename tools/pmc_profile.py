@@ -1,6 +1,6 @@
 """Collect PMC counters for the fused kernel in separate rocprofv3 passes (no tracing domains mixed with --pmc)
 and print per-dispatch medians.  Run on the GPU box from the repo root:
-    python tools/pmc_profile.py [outdir] [-- extra bench.py args]
+    python tools/pmc_profile.py [outdir] [-- extra bench.py args]      (PMC_KERNEL: kernel-name filter, "beamform")
 The parent process never touches the GPU; each pass runs bench.py under rocprofv3 as a child."""
 import csv, glob, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -34,7 +34,7 @@ for i, p in enumerate(PASSES):
     per = {}
     with open(files[0]) as f:
         for row in csv.DictReader(f):
-            if "beamform" not in row.get("Kernel_Name", ""):
+            if os.environ.get("PMC_KERNEL", "beamform") not in row.get("Kernel_Name", ""):
                 continue
             per.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
     for k, v in per.items():
