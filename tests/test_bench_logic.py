@@ -1,0 +1,76 @@
+"""CPU tests of bench.py's bookkeeping and of the timed-region rocprof summary (tools/kernel_stats.py): the real-time
+factor against MeerKAT ingest (BeamformerCoefficientTest.cu:422-465), the kernel named for each workload's roofline,
+the readable kernel names of the per-step split, and that only the dispatches between a region's two marker
+dispatches are summarised (warm-up, clock-settle and contract-check launches excluded)."""
+import csv
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import bench  # noqa: E402
+import kernel_stats  # noqa: E402
+
+
+def test_realtime_factor_against_meerkat_ingest():
+    wl = bench.WORKLOADS["cfg3"]
+    r = bench.realtime(wl, 1, 2475.0)
+    need = 64 * 2 * 4096 * (1712e6 / 8192) / 1e9  # 109.57 Gsamples/s for one 4096-channel band
+    assert r["ingest_need_Gsamples_s"] == pytest.approx(need, abs=0.01)
+    assert r["realtime_factor"] == pytest.approx(2475.0 / need, abs=0.01)
+    r8 = bench.realtime(wl, 8, 8 * 2475.0)  # 8 X-engines: 8x the band, 8x the rate
+    assert r8["ingest_need_Gsamples_s"] == pytest.approx(8 * need, abs=0.1)
+    assert r8["realtime_factor"] == pytest.approx(r["realtime_factor"], abs=0.01)
+
+
+@pytest.mark.parametrize("workload,out_int8,contract,table,expected", [
+    ("cfg3", True, "q14", "on", "beamform_fused_i8_item_kernel"),
+    ("cfg3", True, "f32", "on", "beamform_fused_item_kernel"),
+    ("cfg3", False, "q14", "on", "beamform_fused_item_kernel"),
+    ("cfg2", True, "q14", "on", "beamform_fused_i8_item_kernel"),
+    ("cfg4", True, "q14", "on", "beamform_fused_i8_w32t_kernel"),
+    ("cfg4", True, "q14", "off", "beamform_fused_i8_w32_kernel"),
+    ("cfg4", False, "q14", "on", "beamform_fused_wide_kernel")])
+def test_roofline_kernel_per_workload(workload, out_int8, contract, table, expected):
+    assert bench.kernel_name(bench.WORKLOADS[workload], out_int8, contract, table) == expected
+
+
+def test_short_kernel_names():
+    assert bench.short_kernel("void bf::(anonymous namespace)::q14_table_kernel<false>"
+                              "(bf::(anonymous namespace)::Q14TableArgs)") == "q14_table_kernel<false>"
+    assert bench.short_kernel("void bf::beamform_fused_i8_item_kernel<true, 2, true, 0, 3, true>(bf::FusedArgs)") \
+        == "beamform_fused_i8_item_kernel<true, 2, true, 0, 3, true>"
+
+
+def _trace(path, rows):
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        for name, s, e in rows:
+            w.writerow([name, s, e])
+
+
+def test_timed_regions_keep_only_the_bracketed_dispatches(tmp_path):
+    mark = "bf::bf_trace_mark_kernel(int)"
+    rows = [("warmup_k", 0, 90),                                     # before the first region: excluded
+            (mark, 100, 101), ("k_a", 110, 210), ("k_a", 220, 330), ("gen", 335, 345), (mark, 400, 401),
+            ("contract_check", 410, 900),                            # between regions: excluded
+            (mark, 1000, 1001), ("k_b", 1010, 1060), (mark, 1100, 1101)]
+    p = tmp_path / "trace.csv"
+    _trace(p, rows)
+    regions = kernel_stats.region_stats(str(p))
+    assert len(regions) == 2
+    assert set(regions[0]) == {"k_a", "gen"} and set(regions[1]) == {"k_b"}
+    assert regions[0]["k_a"]["Calls"] == 2 and regions[0]["k_a"]["AverageNs"] == pytest.approx(105.0)
+    name, s = kernel_stats.dominant(regions[0])
+    assert name == "k_a" and s["TotalDurationNs"] == 210
+    assert kernel_stats.dominant(regions[0], "gen")[0] == "gen"
+    out = tmp_path / "stats.csv"
+    kernel_stats.write_csv(regions, str(out))
+    with open(out) as f:
+        got = list(csv.DictReader(f))
+    assert [(r["Region"], r["Name"]) for r in got] == [("0", "k_a"), ("0", "gen"), ("1", "k_b")]
