@@ -93,7 +93,10 @@ def test_q14_coeffs_large_delays(context, command_queue, tau_samples):
     (128, 32, 12, 256, 1, True, True), (96, 24, 5, 16, 3, False, False),
     # 8 k-steps x 2 passes (the straight-line 3-buffer form) with ragged sample chunks, a partial second slab and a
     # ragged last channel group
-    (256, 40, 5, 208, 1, False, True), (256, 64, 6, 144, 2, True, False)])
+    (256, 40, 5, 208, 1, False, True), (256, 64, 6, 144, 2, True, False),
+    # config 4's item shape, signed (64 beams, T = 256: the straight-line 8-step x 2-pass form at A = 256), and 3
+    # k-steps (A = 96) with 64 beams
+    (256, 64, 12, 256, 1, True, False), (256, 64, 9, 256, 2, True, True), (96, 64, 7, 256, 1, True, False)])
 def test_fused_int8_table_path_equals_in_kernel_and_oracle(context, command_queue, A, M, C, T, B, signed, weighted):
     """The int8 wide path with the generated table (default) and with in-kernel phasors (coeff_table=False): the
     same bits, and the integer contract's."""
@@ -122,6 +125,40 @@ def test_fused_int8_table_path_equals_in_kernel_and_oracle(context, command_queu
     np.testing.assert_array_equal(outs[True], outs[False])
     ref = O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, scale=1 / 64, signed=signed, gains=g)
     np.testing.assert_array_equal(outs[True], ref)
+    assert np.abs(ref.astype(int)).max() >= 8
+
+
+def run_int8_wide(context, queue, raw, d, B, C, T, A, M, signed, table, g=None):
+    Ctot, xeng, t0, bdt = 32768, 3, 2e-3, 256 * 2 * 32768 * TS
+    tmpl = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=signed,
+                                   out_int8=True, out_scale=1 / 64, t0=t0, batch_dt=bdt, beam_weights=g is not None,
+                                   coeff_table=table)
+    op = tmpl.instantiate(queue)
+    if g is not None:
+        for m in range(M):
+            op.set_beam_weights(m, g[m])
+    op.ensure_all_bound()
+    op.buffer("inSamples").set(queue, raw)
+    op.buffer("delay_vals").set(queue, d)
+    op()
+    return op.buffer("outData").get(queue)
+
+
+@pytest.mark.parametrize("A,C,B,weighted", [(64, 600, 1, False), (128, 150, 2, True), (32, 270, 1, True),
+                                            (32, 257, 1, False), (256, 300, 1, False)])
+def test_int8_table_path_channel_groups(context, command_queue, A, C, B, weighted):
+    """The table-driven slab kernel at 64 beams and T = 256 over many channels: ragged last 4-channel groups
+    (C % 4 = 1, 2), two batches, 1, 2, 4 and 8 k-steps (A = 32 ... 256), more workgroups than CUs.  Bitwise equal to
+    the in-kernel-phasor slab kernel (itself pinned to the oracle above and in test_gpu_fullsize.py).  (These shapes
+    also pinned the output-stationary LDS-DMA kernel measured in round 3, bf_wide_i8os.hip, diagnostic build.)"""
+    M, T = 64, 256
+    d = delays(1, M, A, seed=A + C)
+    rng = np.random.default_rng(A * 3 + C)
+    raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8).view(np.int8)
+    g = rng.uniform(-1.2, 1.2, (M, A)).astype(np.float32) if weighted else None
+    got = run_int8_wide(context, command_queue, raw, d, B, C, T, A, M, True, True, g)
+    ref = run_int8_wide(context, command_queue, raw, d, B, C, T, A, M, True, False, g)
+    np.testing.assert_array_equal(got, ref)
     assert np.abs(ref.astype(int)).max() >= 8
 
 

@@ -86,14 +86,38 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
     tnames.update({300 + m: v.replace("early ", "") + " [unrolled NB3]" for m, v in base.items()})
     tnames.update({400 + m: v.replace("early ", "") + " [unrolled NB4]" for m, v in base.items()})
     tnames.update({500 + m: v + " [unrolled NB3, early table]" for m, v in base.items()})
+    # 700 + m: the output-stationary LDS-DMA kernel (bf_wide_i8os.hip) on the same table; m = its Mode bits
+    tnames.update({700 + m: v.replace("early ", "") + " [os, LDS-DMA]" for m, v in base.items() if m in (0, 1, 4, 8, 9, 12)})
+    tnames.update({702: "no-mfma [os]", 705: "no table,no-store [os]",
+                   713: "no table,no-store,no-load [os]", 715: "skeleton (barriers, LDS reads, VALU) [os]"})
+    tnames.update({729: "no table/store/load, no LDS frag reads [os]", 745: "no table/store/load, no barrier [os]",
+                   761: "MFMA + epilogue VALU only [os]", 732: "full, no barrier (races) [os]"})
+    # 800 + m: the same kernel's 8-wave, one-workgroup-per-CU form (half items, both slabs per workgroup)
+    tnames.update({800 + m - 700: v.replace("[os", "[os8") for m, v in list(tnames.items()) if 700 <= m < 800})
     if _os.environ.get("W32T_MODES"):
         tnames = {int(m): tnames.get(int(m), str(m)) for m in _os.environ["W32T_MODES"].split(",")}
+    lib.bf_diag_i8_os.argtypes = [I, V, V, V, I, I, I, I, I, V]
+
+    def w32t_call(mode, i):
+        if mode >= 700:
+            return lib.bf_diag_i8_os(mode - 700, bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, tb.ptr, B, C, T, A, M, q.handle)
+        return lib.bf_diag_w32_table(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr, tb.ptr, B, C, T, A, M, Ctot,
+                                     1 / 1712e6, q.handle)
+    for mode in tnames:
+        assert mode < 0 or w32t_call(mode, 0) == 0, mode
+    if 700 in tnames:  # the two kernels' int8 beams on the same input and table: bitwise equal
+        outs = []
+        for mode in (300, 700):
+            _lib.call("bf_memset", bufs[0][1].ptr, 0, nout // 4, q.handle)
+            assert w32t_call(mode, 0) == 0
+            outs.append(bufs[0][1].get(q)[: nout // 4].copy())
+        print(f"  os vs slab kernel int8 beams: {'bitwise equal' if np.array_equal(*outs) else 'DIFFERENT'} "
+              f"({int((outs[0] != outs[1]).sum())} bytes differ)")
     alg8 = nin + nout // 4
     res = {m: [] for m in tnames}
     for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
         for mode in tnames:
-            res[mode].append(timeit(lambda i: lib.bf_diag_w32_table(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
-                                                                    tb.ptr, B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
+            res[mode].append(timeit(lambda i: w32t_call(mode, i)))
     for mode in tnames:
         ts = sorted(res[mode])
         print(f"  w32t mode {mode:3d} {tnames[mode]:28s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
