@@ -19,6 +19,7 @@ struct FusedArgs {
   void* y;
   int delay_channels, B, C, T, A, M, S, NT, nslabs, xcd_order;
   int path, order;  // BF_FUSED_PATH_* and BF_FUSED_ORDER_* bits of the launch flags (0 = automatic)
+  int c_count;      // table-driven int8 path: channels this launch processes (0 = C; strides always use C)
   long long base_ch;
   double ctot, ts, k, t0, batch_dt;
   float out_scale;

@@ -37,7 +37,7 @@ struct Q14TableArgs {
   const float4* dv;
   const float* gain;
   uint32_t* out;
-  int delay_channels, B, C, A, M, Sp, nslabs, layout, run, unit_fast;
+  int delay_channels, B, C, A, M, Sp, nslabs, layout, run, unit_fast, Cn;  // Cn: channels written (a chunk)
   long long base_ch;
   double ctot, ts, k, t0, batch_dt;
 };
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
     words = static_cast<size_t>(per_slab) * P.nslabs;
     base = (static_cast<size_t>(b) * P.C + c0) * words + w;
   }
-  const int nrun = min(P.run, P.C - c0);
+  const int nrun = min(P.run, P.Cn - c0);
   uint32_t* o = P.out + base;
   if (!valid) {
     for (int j = 0; j < nrun; ++j) o[static_cast<size_t>(j) * words] = 0u;
@@ -140,6 +140,7 @@ int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t 
   Q.out = out;
   Q.delay_channels = P.delay_channels;
   Q.B = P.B, Q.C = P.C, Q.A = P.A, Q.M = P.M;
+  Q.Cn = P.c_count ? P.c_count : P.C;
   Q.Sp = w32_table_steps(P.A);
   Q.nslabs = (P.M + 31) / 32;
   Q.layout = layout;
@@ -153,7 +154,7 @@ int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t 
   Q.run = rn ? std::max(1, atoi(rn)) : kQ14Run;
   const char* uf = diag_env("BF_Q14_UNIT");  // measurement: 0 = the two-sided decision for unit gains too
   Q.unit_fast = !(uf && uf[0] == '0');
-  const long long gx = (words + 255) / 256, gy = (P.C + Q.run - 1) / Q.run;
+  const long long gx = (words + 255) / 256, gy = (Q.Cn + Q.run - 1) / Q.run;
   BF_REQUIRE(gx < (1LL << 31) && gy < 65536 && P.B < 65536, "q14 table: grid too large");
   if (P.gain)
     hipLaunchKernelGGL(q14_table_kernel<true>, dim3(static_cast<unsigned>(gx), static_cast<unsigned>(gy), P.B),

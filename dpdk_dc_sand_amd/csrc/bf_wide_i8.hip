@@ -769,7 +769,8 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
-  const int gpb = (P.C + kW32TChannels - 1) / kW32TChannels;  // channel groups per batch
+  const int Cn = P.c_count ? P.c_count : P.C;  // channels of this launch (a chunk: pointers offset by the host)
+  const int gpb = (Cn + kW32TChannels - 1) / kW32TChannels;  // channel groups per batch
   int slab, grp;
   if (P.xcd_order) {  // the slabs of one channel group back to back on one XCD: the second re-reads from L2
     const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
@@ -781,7 +782,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
     grp = blockIdx.x / P.nslabs;
   }
   const int b = grp / gpb, c0 = (grp - b * gpb) * kW32TChannels;
-  const int nk = min(kW32TChannels, P.C - c0);
+  const int nk = min(kW32TChannels, Cn - c0);
   const int m0 = slab * kW32Beams;
   const int Sp = kSp ? kSp : w32_steps(P.A);
   const int T2 = P.T >> 1;
@@ -1013,10 +1014,28 @@ int launch_w32(FusedArgs P, hipStream_t st) {
   const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
   if (P.table && w32_table_fits(P.A) && P.table_bytes >= w32_table_bytes(P.B, P.C, P.A, P.M)) {
-    // the coefficient table of this launch, written by q14_table_kernel just before on `st`
+    // the coefficient table of this launch, written by q14_table_kernel just before on `st`; measurement
+    // (BF_W32_CHUNKS, diagnostic build): generator and contraction alternated over channel chunks
+    const char* ck = diag_env("BF_W32_CHUNKS");
+    const int nchunks = ck ? std::max(1, atoi(ck)) : 1;
+    if (nchunks > 1 && P.B == 1 && P.c_count == 0 && P.delay_channels == 1) {
+      const int per = (P.C + nchunks - 1) / nchunks;
+      for (int c0 = 0; c0 < P.C; c0 += per) {
+        FusedArgs Q = P;
+        Q.c_count = std::min(per, P.C - c0);
+        Q.raw = P.raw + static_cast<size_t>(c0) * P.T * 4;
+        Q.y = static_cast<int8_t*>(P.y) + static_cast<size_t>(c0) * P.T * 2 * P.M;
+        Q.table = P.table + static_cast<size_t>(c0) * ((P.M + 31) / 32) * 1024 * w32_table_steps(P.A);
+        Q.base_ch = P.base_ch + c0;
+        const int e = launch_w32<Signed, Mode>(Q, st);
+        if (e != BF_OK) return e;
+      }
+      return BF_OK;
+    }
     const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32, st);
     if (e != BF_OK) return e;
-    const long long groups = static_cast<long long>(P.B) * ((P.C + kW32TChannels - 1) / kW32TChannels);
+    const int Cn = P.c_count ? P.c_count : P.C;
+    const long long groups = static_cast<long long>(P.B) * ((Cn + kW32TChannels - 1) / kW32TChannels);
     const long long tgrid = P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs;
     const int npasses = ((((P.T >> 1) + 15) >> 4) + 3) >> 2;
     if (w32_steps(P.A) == 8 && npasses == 2)  // config 4's shape: the straight-line 3-buffer ring (386 vs 403 us)
@@ -1129,6 +1148,26 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   }
 #undef BF_W32T
   BF_LAUNCHED("beamform_fused_i8_w32t_kernel");
+}
+
+// The whole table-driven launch (generator + contraction, as bf_beamform_fused_ws runs it); BF_W32_CHUNKS splits it
+// into alternating per-chunk generator / contraction launches.
+extern "C" int bf_diag_w32_launch(const uint8_t* raw, const float* dv, void* y, void* table, int B, int C, int T,
+                                  int A, int M, int Ctot, double ts, void* stream) {
+  bf::FusedArgs P{};
+  P.raw = raw;
+  P.dv = reinterpret_cast<const float4*>(dv);
+  P.y = y;
+  P.table = static_cast<const uint32_t*>(table);
+  P.table_bytes = bf::w32_table_bytes(B, C, A, M);
+  P.delay_channels = 1;
+  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
+  P.ctot = Ctot;
+  P.ts = ts;
+  P.k = -3.141592653589793 / (Ctot * ts);
+  P.batch_dt = 1e-3;
+  P.out_scale = 1.0f / 64;
+  return bf::launch_w32<true, 0>(P, bf::as_stream(stream));
 }
 
 extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y, int B, int C, int T, int A, int M,

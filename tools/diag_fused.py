@@ -122,6 +122,28 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
         ts = sorted(res[mode])
         print(f"  w32t mode {mode:3d} {tnames[mode]:28s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
               f"alg {alg8 / ts[len(ts) // 2] / 1e9:7.1f} GB/s")
+if "w32chunk" in _os.environ.get("DIAG_KERNELS", ""):  # generator + contraction, whole vs channel-chunked launches
+    lib.bf_diag_w32_launch.argtypes = [V, V, V, V, I, I, I, I, I, I, D, V]
+    Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
+    tb2 = accel.DeviceArray(ctx, (B * C * ((M + 31) // 32) * 1024 * 8 + 4096,), np.uint32)
+    chunks = [int(v) for v in _os.environ.get("W32_CHUNKS", "1,2,4,8").split(",")]
+    outs, res = {}, {n: [] for n in chunks}
+    for n in chunks:
+        _os.environ["BF_W32_CHUNKS"] = str(n)
+        _lib.call("bf_memset", bufs[0][1].ptr, 0, nout // 4, q.handle)
+        assert lib.bf_diag_w32_launch(bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, tb2.ptr, B, C, T, A, M, Ctot,
+                                      1 / 1712e6, q.handle) == 0
+        outs[n] = bufs[0][1].get(q)[: nout // 4].copy()
+    print("  chunked == whole launch (int8 beams):", all(np.array_equal(outs[chunks[0]], o) for o in outs.values()))
+    for r in range(ROUNDS):
+        for n in chunks:
+            _os.environ["BF_W32_CHUNKS"] = str(n)
+            res[n].append(timeit(lambda i: lib.bf_diag_w32_launch(bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
+                                                                  tb2.ptr, B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
+    for n in chunks:
+        ts = sorted(res[n])
+        print(f"  generator + contraction, {n} channel chunk(s): median {ts[len(ts) // 2] * 1e6:8.1f} us")
+    _os.environ.pop("BF_W32_CHUNKS")
 if "w8" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_w8.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
     w8names = {0: "full (fast+fixup)", 128: "exact-only coef", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
