@@ -1038,8 +1038,10 @@ int launch_w32(FusedArgs P, hipStream_t st) {
     const long long groups = static_cast<long long>(P.B) * ((Cn + kW32TChannels - 1) / kW32TChannels);
     const long long tgrid = P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs;
     const int npasses = ((((P.T >> 1) + 15) >> 4) + 3) >> 2;
-    if (w32_steps(P.A) == 8 && npasses == 2)  // config 4's shape: the straight-line 3-buffer ring (386 vs 403 us)
-      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false, 8, 2, 3>),
+    // config 4's shape: the straight-line ring, two step buffers (one step in flight while one is contracted):
+    // 377 vs 384 us for three buffers and 403 for the runtime loop (profiles/r3_ab_*, r3_g_*)
+    if (w32_steps(P.A) == 8 && npasses == 2)
+      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false, 8, 2, 2>),
                          dim3(static_cast<unsigned>(tgrid)), dim3(kW8Threads), lds, st, P);
     else
       hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false>), dim3(static_cast<unsigned>(tgrid)),
@@ -1141,6 +1143,7 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   case 100 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
   case 300 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
   case 400 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 4>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 200 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
   case 500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, true, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break
   switch (mode) {
     BF_W32T(0); BF_W32T(1); BF_W32T(4); BF_W32T(8); BF_W32T(9); BF_W32T(12);

@@ -91,7 +91,7 @@ def test_q14_coeffs_large_delays(context, command_queue, tau_samples):
 @pytest.mark.parametrize("A,M,C,T,B,signed,weighted", [
     (256, 64, 24, 64, 1, True, False), (256, 64, 17, 32, 1, False, True), (200, 40, 9, 48, 2, False, False),
     (128, 32, 12, 256, 1, True, True), (96, 24, 5, 16, 3, False, False),
-    # 8 k-steps x 2 passes (the straight-line 3-buffer form) with ragged sample chunks, a partial second slab and a
+    # 8 k-steps x 2 passes (the straight-line 2-buffer form) with ragged sample chunks, a partial second slab and a
     # ragged last channel group
     (256, 40, 5, 208, 1, False, True), (256, 64, 6, 144, 2, True, False),
     # config 4's item shape, signed (64 beams, T = 256: the straight-line 8-step x 2-pass form at A = 256), and 3

@@ -85,6 +85,7 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
     tnames.update({100 + m: v.replace("early", "late") + (" (late)" if m else "") for m, v in base.items()})
     tnames.update({300 + m: v.replace("early ", "") + " [unrolled NB3]" for m, v in base.items()})
     tnames.update({400 + m: v.replace("early ", "") + " [unrolled NB4]" for m, v in base.items()})
+    tnames.update({200 + m: v.replace("early ", "") + " [unrolled NB2: the product form]" for m, v in base.items()})
     tnames.update({500 + m: v + " [unrolled NB3, early table]" for m, v in base.items()})
     # 700 + m: the output-stationary LDS-DMA kernel (bf_wide_i8os.hip) on the same table; m = its Mode bits
     tnames.update({700 + m: v.replace("early ", "") + " [os, LDS-DMA]" for m, v in base.items() if m in (0, 1, 4, 8, 9, 12)})
