@@ -752,9 +752,9 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
 // ---- the table-driven 32-beam kernel (the default with a workspace) -----------------------------------------------
 // The Q14 coefficients come from the launch's table (q14_table_kernel, kLayoutW32: per (b, c, slab) 1024 Sp words,
 // thread tid's units j = tid + 256 j as two 16-byte loads each) instead of phasors evaluated here, and a workgroup
-// walks kW32TChannels consecutive channels of its slab: the next channel's table is requested after the current
-// channel's last MFMAs (its latency under the stores), and the voltage prefetch runs on from one channel into the
-// next, so only a workgroup's first channel starts cold (measured on the one-channel form: a cold start -- table +
+// walks kCh consecutive channels of its slab (kW32TChannels; 8 at config 4's shape): the next channel's table is
+// requested after the current channel's last MFMAs (its latency under the stores), and the voltage prefetch runs on
+// from one channel into the next, so only a workgroup's first channel starts cold (measured on the one-channel form: a cold start -- table +
 // first voltage steps -- per (channel, slab) cost ~50 us of 430 at config 4, profiles/r3_e_w32t_ablation.txt).
 // Mode (diagnostics): 1 no table loads / expansion, 4 no stores, 8 no voltage loads.
 constexpr int kW32TChannels = 4;
@@ -764,13 +764,13 @@ constexpr int kW32TChannels = 4;
 // 16 steps are straight-line code: the four step buffers keep their registers, and the compiler no longer re-homes
 // them through copies behind s_waitcnt vmcnt(22 .. 0) at every loop header -- a full drain of the voltage prefetch
 // every four steps in the runtime-bounded form.
-template <bool Signed, int Mode = 0, bool Early = true, int kSp = 0, int kNP = 0, int kNB = 4>
+template <bool Signed, int Mode = 0, bool Early = true, int kSp = 0, int kNP = 0, int kNB = 4, int kCh = kW32TChannels>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
   const int Cn = P.c_count ? P.c_count : P.C;  // channels of this launch (a chunk: pointers offset by the host)
-  const int gpb = (Cn + kW32TChannels - 1) / kW32TChannels;  // channel groups per batch
+  const int gpb = (Cn + kCh - 1) / kCh;  // channel groups per batch
   int slab, grp;
   if (P.xcd_order) {  // the slabs of one channel group back to back on one XCD: the second re-reads from L2
     const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
@@ -781,8 +781,8 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
     slab = blockIdx.x % P.nslabs;
     grp = blockIdx.x / P.nslabs;
   }
-  const int b = grp / gpb, c0 = (grp - b * gpb) * kW32TChannels;
-  const int nk = min(kW32TChannels, Cn - c0);
+  const int b = grp / gpb, c0 = (grp - b * gpb) * kCh;
+  const int nk = min(kCh, Cn - c0);
   const int m0 = slab * kW32Beams;
   const int Sp = kSp ? kSp : w32_steps(P.A);
   const int T2 = P.T >> 1;
@@ -1035,13 +1035,16 @@ int launch_w32(FusedArgs P, hipStream_t st) {
     const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32, st);
     if (e != BF_OK) return e;
     const int Cn = P.c_count ? P.c_count : P.C;
-    const long long groups = static_cast<long long>(P.B) * ((Cn + kW32TChannels - 1) / kW32TChannels);
-    const long long tgrid = P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs;
     const int npasses = ((((P.T >> 1) + 15) >> 4) + 3) >> 2;
+    // config 4's shape walks 8 channels per workgroup (385.5 vs 389.4 us for 4, profiles/r3_ad*), the others 4
+    const bool straight = w32_steps(P.A) == 8 && npasses == 2;
+    const int ch = straight ? 8 : kW32TChannels;
+    const long long groups = static_cast<long long>(P.B) * ((Cn + ch - 1) / ch);
+    const long long tgrid = P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs;
     // config 4's shape: the straight-line ring, two step buffers (one step in flight while one is contracted):
     // 377 vs 384 us for three buffers and 403 for the runtime loop (profiles/r3_ab_*, r3_g_*)
-    if (w32_steps(P.A) == 8 && npasses == 2)
-      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false, 8, 2, 2>),
+    if (straight)
+      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false, 8, 2, 2, 8>),
                          dim3(static_cast<unsigned>(tgrid)), dim3(kW8Threads), lds, st, P);
     else
       hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false>), dim3(static_cast<unsigned>(tgrid)),
@@ -1138,12 +1141,19 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   const long long groups = static_cast<long long>(B) * ((C + bf::kW32TChannels - 1) / bf::kW32TChannels);
   const unsigned grid = static_cast<unsigned>(P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs);
   const size_t lds = bf::w32_lds_bytes(A);
+  auto grid_for = [&](int ch) {  // channels per workgroup other than kW32TChannels (measurement)
+    const long long g = static_cast<long long>(B) * ((C + ch - 1) / ch);
+    return static_cast<unsigned>(P.xcd_order ? (g + 7) / 8 * 8 * P.nslabs : g * P.nslabs);
+  };
 #define BF_W32T(m) \
   case m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
   case 100 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
   case 300 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
   case 400 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 4>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
   case 200 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 220 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 2>), dim3(grid_for(2)), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 240 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 260 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 16>), dim3(grid_for(16)), dim3(bf::kW8Threads), lds, st, P); break; \
   case 500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, true, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break
   switch (mode) {
     BF_W32T(0); BF_W32T(1); BF_W32T(4); BF_W32T(8); BF_W32T(9); BF_W32T(12);
