@@ -147,8 +147,9 @@ def run_int8_wide(context, queue, raw, d, B, C, T, A, M, signed, table, g=None):
 @pytest.mark.parametrize("A,C,B,weighted", [(64, 600, 1, False), (128, 150, 2, True), (32, 270, 1, True),
                                             (32, 257, 1, False), (256, 300, 1, False)])
 def test_int8_table_path_channel_groups(context, command_queue, A, C, B, weighted):
-    """The table-driven slab kernel at 64 beams and T = 256 over many channels: ragged last 4-channel groups
-    (C % 4 = 1, 2), two batches, 1, 2, 4 and 8 k-steps (A = 32 ... 256), more workgroups than CUs.  Bitwise equal to
+    """The table-driven slab kernel at 64 beams and T = 256 over many channels: ragged last channel groups (4 per
+    workgroup, C % 4 = 1, 2; 8 at A = 256, C % 8 = 4), two batches, 1, 2, 4 and 8 k-steps (A = 32 ... 256), more
+    workgroups than CUs.  Bitwise equal to
     the in-kernel-phasor slab kernel (itself pinned to the oracle above and in test_gpu_fullsize.py).  (These shapes
     also pinned the output-stationary LDS-DMA kernel measured in round 3, bf_wide_i8os.hip, diagnostic build.)"""
     M, T = 64, 256
