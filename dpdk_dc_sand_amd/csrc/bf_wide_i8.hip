@@ -1154,6 +1154,7 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   case 220 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 2>), dim3(grid_for(2)), dim3(bf::kW8Threads), lds, st, P); break; \
   case 240 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
   case 260 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 16>), dim3(grid_for(16)), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 280 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, true, 8, 2, 2, 8>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
   case 500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, true, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break
   switch (mode) {
     BF_W32T(0); BF_W32T(1); BF_W32T(4); BF_W32T(8); BF_W32T(9); BF_W32T(12);

@@ -86,7 +86,8 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
     tnames.update({300 + m: v.replace("early ", "") + " [unrolled NB3]" for m, v in base.items()})
     tnames.update({400 + m: v.replace("early ", "") + " [unrolled NB4]" for m, v in base.items()})
     tnames.update({200 + m: v.replace("early ", "") + " [unrolled NB2: the product form]" for m, v in base.items()})
-    tnames.update({220: "full [NB2, 2 ch/WG]", 240: "full [NB2, 8 ch/WG]", 260: "full [NB2, 16 ch/WG]"})
+    tnames.update({220: "full [NB2, 2 ch/WG]", 240: "full [NB2, 8 ch/WG]", 260: "full [NB2, 16 ch/WG]",
+                   280: "full [NB2, 8 ch/WG, early table]"})
     tnames.update({500 + m: v + " [unrolled NB3, early table]" for m, v in base.items()})
     # 700 + m: the output-stationary LDS-DMA kernel (bf_wide_i8os.hip) on the same table; m = its Mode bits
     tnames.update({700 + m: v.replace("early ", "") + " [os, LDS-DMA]" for m, v in base.items() if m in (0, 1, 4, 8, 9, 12)})
@@ -107,7 +108,7 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
                                      1 / 1712e6, q.handle)
     for mode in tnames:
         assert mode < 0 or w32t_call(mode, 0) == 0, mode
-    for alt in (220, 240, 260, 700):  # another kernel form's int8 beams on the same input and table: bitwise equal
+    for alt in (220, 240, 260, 280, 700):  # another kernel form's int8 beams on the same input and table: bitwise equal
         if alt not in tnames:
             continue
         outs = []
