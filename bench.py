@@ -24,7 +24,8 @@ runs libbf on one HIP runtime.  At N > 1 the line's `secondary` also times confi
 Rank 0 prints ONE JSON line.  `value` = samples all ranks processed / max-over-ranks wall time of the K timed
 steps (barrier + device sync on both sides).  `roofline.achieved` = algorithmic bytes per launch / average
 launch duration from HIP events on the launch stream; `roofline.read_frac` = the voltage bytes alone / that time /
-peak (the north star's "HBM-read roofline").  `roofline.traffic` = HBM bytes per launch from rocprofv3 PMC
+peak (the north star's "HBM-read roofline"), and `read_frac_ceiling` the same for this box's plain streaming kernel
+over the kernel's whole read + write byte mix: the read fraction the beams' writes leave reachable.  `roofline.traffic` = HBM bytes per launch from rocprofv3 PMC
 counters (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate passes), rank 0, N = 1.  `ceiling` = the same
 traffic mix as a plain streaming kernel on this box (diagnostic library), when it is built.
 `cpu_baseline` = the oracle's vectorised NumPy restatement on a bounded channel sample, rank 0, N = 1.
@@ -157,17 +158,17 @@ def scatter_inputs(args, dist, shape):
     report = {"backend": dist.scatter_backend, "bytes_per_rank": per_rank, "ranks": world,
               "band_shape": [B, A, C * world, T, 2, 2]}
     if dist.scatter_backend == "rccl":
-        dist.open_comm(args.ctx)
         band, err = None, None
-        try:
+        try:  # every rank's buffers first: the communicator's set-up is a blocking collective
             if rank == 0:
                 band = accel.DeviceArray(args.ctx, (B, A, C * world, T, 2, 2), dt)
                 _lib.call("bf_fill_random", band.ptr, band.nbytes, 1, args.queue.handle)
             out = accel.DeviceArray(args.ctx, shape, dt)
         except Exception as e:  # noqa: BLE001
             err = e
-        if dist.max(1.0 if err else 0.0) > 0:  # agree before any rank posts its ncclRecv
+        if dist.max(1.0 if err else 0.0) > 0:  # agree before any rank enters bf_comm_create or posts its ncclRecv
             raise err or RuntimeError("scatter set-up failed on another rank")
+        dist.open_comm(args.ctx)
         times = []
         for _ in range(3):
             args.queue.finish()
@@ -176,10 +177,18 @@ def scatter_inputs(args, dist, shape):
             dist.comm.scatter(band, out, B, A, C, T, args.queue)
             args.queue.finish()
             times.append(time.perf_counter() - t0)
-        del band
         t = dist.max(min(times))
+        # what arrived is what the root sent: per-rank slice checksums against the root's band (on the devices)
+        ok, per_rank = dist.comm.verify(band, out, B, A, C, T, args.queue)
+        sent, received = dist.comm.stats()
+        del band
+        report["verified"] = ok
+        if per_rank is not None:
+            report["checksums"] = per_rank
+        report["rccl_bytes_received_this_rank"] = received
+        report["rccl_bytes_sent_root"] = sent if rank == 0 else None
         report["collective"] = ("RCCL grouped ncclSend/ncclRecv over xGMI via libbf bf_channel_scatter, device to "
-                                "device (root: one 2-D pack per peer)")
+                                "device (root: one 2-D pack per rank, its own slice by a self send/recv)")
     else:
         full = None
         if rank == 0:
@@ -341,45 +350,70 @@ def stream_ceiling(args, in_bytes, out_bytes):
             "note": "best plain streaming kernel over the same read/write byte mix on this box"}
 
 
-def cpu_baseline(wl, out_int8, seconds=10.0):
-    """The oracle's vectorised NumPy restatement (reorder -> per-batch coefficients -> f32 matmul) timed on
-    this host on a bounded channel sample of the same workload (kind "port")."""
-    import numpy as np
-
-    import oracle as O
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-    except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
-    A, M, T, B = wl["A"], wl["M"], wl["T"], wl["B"]
-    rng = np.random.default_rng(7)
-    d = np.zeros((1, M, A, 4), np.float32)
-    d[..., 0] = rng.uniform(0, 10 * TS, d.shape[:-1])
-    d[..., 2] = rng.uniform(-np.pi, np.pi, d.shape[:-1])
-
-    def once(c):
-        raw = rng.integers(-128, 128, size=(B, A, c, T, 2, 2), dtype=np.int8)
-        t = time.perf_counter()
-        Ctot = wl.get("Ctot", wl["C"])
-        y = O.fused_beamform(raw, d, Ctot, signed=True, batch_dt=T * 2 * Ctot * TS)
-        if out_int8:
-            O.requantise(y, 1 / 64)
-        return time.perf_counter() - t
-
-    c = 16
-    dt = once(c)  # warm-up + rate estimate
-    c = int(min(max(16, c * seconds / max(dt, 1e-3)), wl["C"]))
-    dt = once(c)
-    rate = A * 2 * c * T * B / dt / 1e9
+def host_cpus():
+    """(CPUs in this process's affinity mask, the cgroup CPU quota in cores or None)."""
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover - non-Linux
         affinity = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return int(affinity), quota
+
+
+def cpu_baseline(wl, out_int8, seconds=10.0):
+    """The oracle's vectorised NumPy restatement (reorder -> per-batch coefficients -> f32 matmul) timed on
+    this host on a bounded channel sample of the same workload (kind "port"): the same delay model as the timed GPU
+    run (bench.delay_model: delays, delay rates, phases, phase rates), BLAS threads = every CPU in the affinity
+    mask (the baseline uses the host's cores; `cores` is that thread count)."""
+    import numpy as np
+
+    import oracle as O
+    affinity, quota = host_cpus()
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(limits=affinity, user_api="blas")
+    except Exception:  # noqa: BLE001 -- threadpoolctl missing: the BLAS default (reported below)
+        limiter = None
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:  # noqa: BLE001
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    A, M, T, B = wl["A"], wl["M"], wl["T"], wl["B"]
+    Ctot = wl.get("Ctot", wl["C"])
+    rng = np.random.default_rng(7)
+    d = delay_model(np, rng, (1, M, A, 4))
+
+    def once(c):
+        raw = rng.integers(-128, 128, size=(B, A, c, T, 2, 2), dtype=np.int8)
+        t = time.perf_counter()
+        y = O.fused_beamform(raw, d, Ctot, signed=True, t0=0.0, batch_dt=T * 2 * Ctot * TS)
+        if out_int8:
+            O.requantise(y, 1 / 64)
+        return time.perf_counter() - t
+
+    try:
+        c = 16
+        once(c)  # warm-up
+        dt = once(c)  # rate estimate
+        c = int(min(max(16, c * seconds / max(dt, 1e-3)), wl["C"]))
+        dt = once(c)
+    finally:
+        if limiter is not None:
+            limiter.unregister()
+    rate = A * 2 * c * T * B / dt / 1e9
     return {"value": round(rate, 4), "unit": "Gsamples/s", "cores": int(threads), "blas_threads": int(threads),
-            "host_cpus_in_affinity": int(affinity), "kind": "port",
-            "sample": f"{c} of {wl['C']} channels x B={B} x T={T} x A={A} x 2 pols ({dt:.1f} s): oracle.fused_beamform "
-                      f"(NumPy reorder + float64-phase coefficients + float32 matmul{' + requantise' if out_int8 else ''}, "
+            "host_cpus_in_affinity": affinity, "cgroup_cpu_quota_cores": quota, "kind": "port",
+            "sample": f"{c} of {wl['C']} channels x B={B} x T={T} x A={A} x 2 pols ({dt:.1f} s), extrapolated "
+                      f"linearly in channels: oracle.fused_beamform (NumPy reorder + float64-phase coefficients "
+                      f"with delay/phase rates + float32 matmul{' + requantise' if out_int8 else ''}, "
                       f"BLAS threads={threads})"}
 
 
@@ -549,6 +583,7 @@ def secondary(args, dist, workload, out_int8, int8_contract="q14"):
         if ceil:
             out["ceiling"] = ceil
             out["frac_of_ceiling"] = round(ceil["us"] / out["avg_launch_us"], 4)
+            out["read_frac_ceiling"] = round(r["read_bytes"] / (ceil["us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     return out
 
 
@@ -581,6 +616,8 @@ def main():
             inputs = None
             scatter = {"backend": dist.scatter_backend, "error": err or "failed on another rank",
                        "note": "scatter failed; each rank generated its shard in place"}
+    # top level, so a failed or unverified collective cannot pass for a clean scaling point (None: no scatter)
+    scatter_ok = None if scatter is None else ("error" not in scatter and scatter.get("verified", True) is not False)
     r = run_gpu(args, dist, wl, tmpl=tmpl, inputs=inputs)
     total_samples = r["samples_per_step"] * args.steps * dist.world
     value = total_samples / r["t_max"] / 1e9
@@ -605,6 +642,7 @@ def main():
                      "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"],
                      "read_bytes_per_launch": r["read_bytes"]},
         "mfma": mfma_util(wl, args.out_int8, args.int8_contract, r["kernel_s"]),
+        "scatter_ok": scatter_ok,
         "scatter": scatter or {"backend": None, "note": "no scatter: single rank, or --scatter-backend none "
                                                         "(each rank generates its shard in place)"},
         "realtime": realtime(wl, dist.world, value),
@@ -618,6 +656,9 @@ def main():
         if ceil:
             line["ceiling"] = ceil
             line["roofline"]["frac_of_ceiling"] = round(ceil["us"] / line["roofline"]["avg_launch_us"], 4)
+            # the north star's "HBM-read roofline": with the beams written too, a read-only fraction of 1 is not
+            # reachable; the best this box allows is the voltage bytes over its own stream time for the same mix
+            line["roofline"]["read_frac_ceiling"] = round(r["read_bytes"] / (ceil["us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     if not args.no_secondary and args.workload == "cfg3":
         # every rank runs the secondaries (each is timed between barriers, max over ranks); at N > 1 config 4
         # channel-sharded: 4096 channels per rank of the 32768-channel band (BASELINE configs[3] at N = 8)

@@ -81,6 +81,9 @@ PROTOTYPES = {
     "bf_comm_destroy": (c_int, [c_void_p]),
     "bf_comm_allreduce_max": (c_int, [c_void_p, ctypes.POINTER(c_double)]),
     "bf_channel_scatter": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "bf_comm_stats": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]),
+    "bf_comm_load": (c_int, []),
+    "bf_checksum": (c_int, [c_void_p, c_size_t, c_size_t, c_size_t, ctypes.POINTER(ctypes.c_ulonglong), c_void_p]),
     "bf_fill_random": (c_int, [c_void_p, c_size_t, ctypes.c_ulonglong, c_void_p]),
 }
 
@@ -88,7 +91,7 @@ PROTOTYPES = {
 # bf_beamform_fused flags (include/bf.h)
 FUSED_SIGNED, FUSED_OUT_INT8, FUSED_EXACT_COEFF, FUSED_INT8_VIA_F32 = 1, 2, 4, 8
 # kernel-path / workgroup-order overrides (tests and measurement; every path computes the same contract)
-FUSED_PATH = {"auto": 0, "item": 0x100, "generic": 0x300, "wide": 0x400, "wide16": 0x500}
+FUSED_PATH = {"auto": 0, "item": 0x100, "generic": 0x300, "wide": 0x400}
 FUSED_ORDER = {"auto": 0, "channel": 0x1000, "xcd": 0x2000}
 
 

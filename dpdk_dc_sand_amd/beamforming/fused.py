@@ -41,7 +41,7 @@ class FusedBeamformerTemplate:
     beam_weights: carry a per-(beam, input) real weight table (slot beamWeights, set with set_beam_weights).
     int8_contract: with out_int8, "q14" (default: the integer contract, Q14 coefficients and exact int32 sums on the
         integer MFMA path) or "f32" (requantised float32 beams: the reference's float32 coefficient arithmetic).
-    kernel_path, workgroup_order: force a kernel path ("auto", "item", "generic", "wide", "wide16") or
+    kernel_path, workgroup_order: force a kernel path ("auto", "item", "generic", "wide") or
         workgroup order ("auto", "channel", "xcd") -- tests and measurement; every path computes the same contract.
     coeff_table: let the int8 wide path (many antennas x beams, e.g. config 4) take its Q14 coefficients from a
         table generated just before each launch by the wavefront-parallel phasor kernel (bf_beamform_fused_ws: a

@@ -187,7 +187,9 @@ extern "C" int bf_coeff_gen(const float* delay_vals, float* out, int B, int P, i
   BF_REQUIRE(static_cast<long long>(A) * M < (1LL << 31) && C < 65536, "bf_coeff_gen: shape too large");
   const char* form = bf::diag_env("BF_COEFF_FORM");  // measurement: "thread" / "tile" = the per-(a, m) kernels
   const int na = bf::coef_block_ants(A, M);
-  if (!form && na >= 1) {
+  // the block form stores 16-byte pieces (every antenna pair's rows start 16 M bytes apart): it needs a 16-byte
+  // aligned table; an 8-byte aligned one (a C-ABI caller's offset pointer) takes the per-(a, m) kernels below
+  if (!form && na >= 1 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
     const unsigned gx = static_cast<unsigned>((A + na - 1) / na);
     const size_t lds = static_cast<size_t>(na) * (M + 1) * 16;
     const char* nt = bf::diag_env("BF_COEFF_NT");

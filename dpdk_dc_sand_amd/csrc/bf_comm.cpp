@@ -5,11 +5,15 @@
 // host thread per device (utilities/pcie_bandwidth_tests/main.cpp:193-224, cudaPcieRateTest.cpp:9).  Here one
 // process drives one GPU (rank r = X-engine r) and the root hands every rank its channel slice of a full-band
 // voltage cube once, device to device over xGMI:
-//   root: each peer's slice (B * A strided runs of C*T*4 bytes in the (B, A, C*N, T, 2, 2) band) is packed into a
-//         contiguous staging block by one 2-D copy (the root's own slice straight into its output), then one
-//         grouped ncclSend per peer -- each peer's bytes travel on their own xGMI link at once;
+//   root: every rank's slice (B * A strided runs of C*T*4 bytes in the (B, A, C*N, T, 2, 2) band) is packed into a
+//         contiguous staging block by one 2-D copy, then one RCCL group: a ncclSend per rank -- each peer's bytes
+//         on their own xGMI link at once -- and the root's own ncclRecv of its slice (a self send/recv, so the
+//         same RCCL point-to-point path runs at one rank as at N: the one-GPU box exercises it);
 //   peers: one ncclRecv of the whole slice into the (B, A, C, T, 2, 2) input buffer of the fused beamformer.
-// Everything is ordered on the caller's stream; nothing on the beamforming hot path touches RCCL.
+// Everything is ordered on the caller's stream; nothing on the beamforming hot path touches RCCL.  Every rank
+// records `done` after its part of each scatter; bf_comm_destroy waits for it before tearing the communicator down.
+// bf_checksum (position-weighted 64-bit sum of a 2-D byte region) lets the ranks verify what they received against
+// the root's band without moving it to the host.
 //
 // RCCL is loaded at first use (dlopen of /opt/rocm's librccl.so.1, the ROCm release libbf is built against), so a
 // single-GPU user of libbf never maps it.
@@ -97,6 +101,9 @@ struct bf_comm {
   double* d_scalar = nullptr;  // allreduce scratch
   hipStream_t stream = nullptr;
   hipEvent_t sent = nullptr;   // root: recorded after the last scatter's sends (the staging buffer's last reader)
+  hipEvent_t done = nullptr;   // every rank: recorded after its part of the last scatter (teardown waits for it)
+  bool pending = false;        // a scatter was enqueued since the last wait on `done`
+  unsigned long long p2p_sent = 0, p2p_received = 0;  // bytes handed to ncclSend / ncclRecv
 };
 
 namespace {
@@ -140,8 +147,10 @@ int bf_comm_create(bf_comm** out, const void* id, size_t len, int nranks, int ra
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_scalar), sizeof(double));
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sent, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e != hipSuccess) {
     if (c->d_scalar) (void)hipFree(c->d_scalar);
+    if (c->sent) (void)hipEventDestroy(c->sent);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return bf::hip_fail(e, "bf_comm_create");
@@ -152,6 +161,7 @@ int bf_comm_create(bf_comm** out, const void* id, size_t len, int nranks, int ra
   if (r != ncclSuccess) {
     (void)hipFree(c->d_scalar);
     (void)hipEventDestroy(c->sent);
+    (void)hipEventDestroy(c->done);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return rccl_fail(r, "ncclCommInitRank");
@@ -166,14 +176,15 @@ int bf_comm_destroy(bf_comm* c) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(c->device);
+  // every scatter this rank enqueued (sends, receives, the staging reads) has finished before RCCL is torn down
+  if (c->pending) (void)hipEventSynchronize(c->done);
+  if (c->staging) (void)hipEventSynchronize(c->sent);
   (void)hipStreamSynchronize(c->stream);
   const ncclResult_t r = c->comm ? rccl().comm_destroy(c->comm) : ncclSuccess;
-  if (c->staging) {
-    (void)hipEventSynchronize(c->sent);
-    (void)hipFree(c->staging);
-  }
+  if (c->staging) (void)hipFree(c->staging);
   (void)hipFree(c->d_scalar);
   (void)hipEventDestroy(c->sent);
+  (void)hipEventDestroy(c->done);
   (void)hipStreamDestroy(c->stream);
   delete c;
   if (prev >= 0) (void)hipSetDevice(prev);
@@ -204,7 +215,7 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
   const size_t rows = static_cast<size_t>(B) * A;
   const size_t slice_bytes = run * rows;
   if (c->rank == root) {
-    const size_t need = slice_bytes * static_cast<size_t>(c->nranks - 1);
+    const size_t need = slice_bytes * static_cast<size_t>(c->nranks);
     if (need > c->staging_bytes) {
       if (c->staging) {
         BF_HIP(hipEventSynchronize(c->sent));
@@ -218,27 +229,40 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
     // the previous scatter's sends may still read the staging buffer on another stream
     BF_HIP(hipStreamWaitEvent(st, c->sent, 0));
     uint8_t* stg = static_cast<uint8_t*>(c->staging);
-    for (int r = 0, k = 0; r < c->nranks; ++r) {
-      uint8_t* dst = r == root ? slice : stg + slice_bytes * static_cast<size_t>(k++);
-      BF_HIP(hipMemcpy2DAsync(dst, run, band + run * static_cast<size_t>(r), pitch, run, rows,
-                              hipMemcpyDeviceToDevice, st));
-    }
-    if (c->nranks == 1) return BF_OK;
+    for (int r = 0; r < c->nranks; ++r)
+      BF_HIP(hipMemcpy2DAsync(stg + slice_bytes * static_cast<size_t>(r), run, band + run * static_cast<size_t>(r),
+                              pitch, run, rows, hipMemcpyDeviceToDevice, st));
     BF_RCCL(rccl().group_start());
-    for (int r = 0, k = 0; r < c->nranks; ++r) {
-      if (r == root) continue;
-      const ncclResult_t e = rccl().send(stg + slice_bytes * static_cast<size_t>(k++), slice_bytes, ncclUint8, r,
-                                         c->comm, st);
+    for (int r = 0; r < c->nranks; ++r) {
+      ncclResult_t e = rccl().send(stg + slice_bytes * static_cast<size_t>(r), slice_bytes, ncclUint8, r, c->comm, st);
+      if (e == ncclSuccess && r == root) e = rccl().recv(slice, slice_bytes, ncclUint8, root, c->comm, st);
       if (e != ncclSuccess) {
         (void)rccl().group_end();
-        return rccl_fail(e, "ncclSend");
+        return rccl_fail(e, r == root ? "ncclSend/ncclRecv (self)" : "ncclSend");
       }
     }
     BF_RCCL(rccl().group_end());
     BF_HIP(hipEventRecord(c->sent, st));
+    c->p2p_sent += slice_bytes * static_cast<unsigned long long>(c->nranks);
   } else {
     BF_RCCL(rccl().recv(slice, slice_bytes, ncclUint8, root, c->comm, st));
   }
+  c->p2p_received += slice_bytes;
+  BF_HIP(hipEventRecord(c->done, st));
+  c->pending = true;
+  bf::clear_error();
+  return BF_OK;
+}
+
+int bf_comm_stats(const bf_comm* c, unsigned long long* sent, unsigned long long* received) {
+  BF_REQUIRE(c != nullptr && sent != nullptr && received != nullptr, "bf_comm_stats: null pointer");
+  *sent = c->p2p_sent;
+  *received = c->p2p_received;
+  return BF_OK;
+}
+
+int bf_comm_load(void) {
+  BF_RCCL_LOADED();
   bf::clear_error();
   return BF_OK;
 }

@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "../../include/bf.h"
@@ -68,8 +69,7 @@ inline const char* fused_flags_error(int flags) {
                 BF_FUSED_PATH_MASK | BF_FUSED_ORDER_MASK))
     return "unknown flags";
   const int path = flags & BF_FUSED_PATH_MASK;
-  if (path != 0 && path != BF_FUSED_PATH_ITEM && path != BF_FUSED_PATH_GENERIC && path != BF_FUSED_PATH_WIDE &&
-      path != BF_FUSED_PATH_WIDE16)
+  if (path != 0 && path != BF_FUSED_PATH_ITEM && path != BF_FUSED_PATH_GENERIC && path != BF_FUSED_PATH_WIDE)
     return "unknown kernel path";
   if ((flags & BF_FUSED_ORDER_MASK) == BF_FUSED_ORDER_MASK) return "unknown workgroup order";
   return nullptr;

@@ -548,7 +548,7 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P
   }
   __syncthreads();
   const int4* fr = reinterpret_cast<const int4*>(lds);
-  const float s32 = P.out_scale * 0x1p-14f;  // exact: power-of-two scaling
+  const float s32 = P.out_scale * 0x1p-14f;  // exact: power-of-two scaling (the float rounding of scale is the oracle's)
 
   for (int chunk = wave; chunk < nchunks; chunk += kWaves) {
     const int tq = chunk * 16 + tl;
@@ -840,7 +840,11 @@ __device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, in
       uint32_t q[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = __fadd_rn(__fmul_rn(acc[i][tau][r], s), kMagic);
+        float v;
+        {
+#pragma clang fp contract(off)  // RN(y * s), then the magic add: two roundings (see requant_bits)
+          v = acc[i][tau][r] * s + kMagic;
+        }
         q[r] = __float_as_uint(__builtin_amdgcn_fmed3f(v, kMagic - 127.0f, kMagic + 127.0f));
       }
       pk[tau][i] = pack_low_bytes(q[0], q[1], q[2], q[3]);
@@ -1145,10 +1149,9 @@ int launch_i8(FusedArgs P, hipStream_t st) {
   const int S8 = (2 * P.A + 63) / 64;
   const int choice = fused_kernel_choice(P);
   const bool small = S8 <= 2 && P.T <= 256;
+  // the 32-beam slab kernels up to A = 512 (their Q14 limb image in LDS); beyond, the generic kernel (groups of 64
+  // antennas).  (The round-1 16-beam slab kernel, which also covered 512 < A <= 724, is in the diagnostic build only.)
   if ((choice == BF_FUSED_PATH_WIDE || (choice == 0 && !small)) && i8_w32_fits(P)) return launch_i8_w32<Signed>(P, st);
-  if ((choice == BF_FUSED_PATH_WIDE || choice == BF_FUSED_PATH_WIDE16 ||
-       (choice == 0 && !small)) && i8_wide_fits(P))
-    return launch_i8_wide<Signed>(P, st);
   if (small && choice != BF_FUSED_PATH_GENERIC) {
     const int M2 = 2 * P.M;
     if (P.NT >= 2) {
@@ -1210,8 +1213,7 @@ int dispatch(FusedArgs P, hipStream_t st) {
   const bool small = P.S <= kGroup && P.T <= 256;
   if constexpr (!OutI8) {
     // many antennas x beams (config 4): the wide kernel keeps every beam of the item in one workgroup
-    const bool wide = choice == BF_FUSED_PATH_WIDE || choice == BF_FUSED_PATH_WIDE16 ||
-                      (choice == 0 && P.M >= 24 && (!small || P.M > 32));
+    const bool wide = choice == BF_FUSED_PATH_WIDE || (choice == 0 && P.M >= 24 && (!small || P.M > 32));
     if (wide && wide_fits(P)) return launch_wide<Signed, Exact>(P, st);
   }
   if (small && choice != BF_FUSED_PATH_GENERIC) {

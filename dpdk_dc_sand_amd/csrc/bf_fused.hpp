@@ -53,10 +53,29 @@ __device__ __forceinline__ int coef8_byte(int k, int cl, int nts, int limb) {
 // half to even), and v_med3 against 1.5 * 2^23 +- 127 clamps every larger value to the right end.  The low byte of
 // the clamped bits is then q in two's complement: 3 VALU + a quarter of a pack per value, instead of
 // rint + clamp + float->int + shift/or (7).
+// The two roundings are the contract: RN(y * s) first, then the magic add.  __fmul_rn / __fadd_rn alone do not stop
+// hipcc from contracting them into one v_fma (v_fmaak_f32: a single rounding of y * s + magic, which differs where
+// y * s lies within half a float32 ulp of a half-integer), so contraction is switched off here.  Pow2 = true: the
+// caller guarantees s is a power of two, so y * s is exact and the single FMA is the same value (one VALU less).
+template <bool Pow2 = false>
 __device__ __forceinline__ uint32_t requant_bits(int y, float s) {
   constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
-  const float v = __fadd_rn(__fmul_rn(static_cast<float>(y), s), kMagic);
+  float v;
+  if constexpr (Pow2) {
+    v = __builtin_fmaf(static_cast<float>(y), s, kMagic);
+  } else {
+#pragma clang fp contract(off)
+    v = static_cast<float>(y) * s + kMagic;
+  }
   return __float_as_uint(__builtin_amdgcn_fmed3f(v, kMagic - 127.0f, kMagic + 127.0f));
+}
+
+// Whether s is a power of two (a normal float with an all-zero mantissa): requant_bits<true> is then exact.
+inline bool scale_is_pow2(float s) {
+  uint32_t u;
+  memcpy(&u, &s, 4);
+  const uint32_t e = (u >> 23) & 255;
+  return (u & 0x7fffffu) == 0 && e > 0 && e < 255;
 }
 
 // [a.b0, b.b0, c.b0, d.b0]: three v_perm_b32
@@ -104,11 +123,8 @@ inline size_t w32_table_bytes(int B, int C, int A, int M) {
 }
 int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t st);
 
-// Integer wide kernels: int8 beams for many antennas x beams.  bf_wide_i8.hip: a workgroup per 32-beam slab (the
-// default, BF_FUSED_PATH_WIDE) or per 16-beam slab (BF_FUSED_PATH_WIDE16).
-bool i8_wide_fits(const FusedArgs& P);
-template <bool Signed>
-int launch_i8_wide(FusedArgs P, hipStream_t st);
+// Integer wide kernels: int8 beams for many antennas x beams.  bf_wide_i8.hip: a workgroup per 32-beam slab
+// (BF_FUSED_PATH_WIDE, and the automatic path beyond the item kernel's shapes).
 bool i8_w32_fits(const FusedArgs& P);
 template <bool Signed>
 int launch_i8_w32(FusedArgs P, hipStream_t st);

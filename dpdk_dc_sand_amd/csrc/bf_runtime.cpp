@@ -46,6 +46,23 @@ __global__ __launch_bounds__(256) void bf_fill_random_kernel(uint8_t* dst, size_
   }
 }
 
+// Position-weighted checksum of a 2-D region of 4-byte words (rows x run_words, row pitch pitch_words): the sum
+// over packed word index i of splitmix64(splitmix64(i) ^ w_i), mod 2^64.  The same value for a contiguous slice and
+// for the strided band region it was packed from (bf_channel_scatter verification).
+__global__ __launch_bounds__(256) void bf_checksum_kernel(const uint32_t* p, size_t run_words, size_t pitch_words,
+                                                          size_t rows, unsigned long long* out) {
+  unsigned long long h = 0;
+  for (size_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    const uint32_t* row = p + r * pitch_words;
+    for (size_t j = blockIdx.x * 256ull + threadIdx.x; j < run_words; j += static_cast<size_t>(gridDim.x) * 256) {
+      const unsigned long long i = r * run_words + j;
+      h += splitmix64(splitmix64(i) ^ row[j]);
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) h += __shfl_xor(h, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, h);
+}
+
 int cu_count() {
   static std::atomic<int> cache[64];  // per device index; 0 = not looked up yet
   int dev = 0, n = 0;
@@ -205,6 +222,33 @@ int bf_fill_random(void* dst, size_t bytes, unsigned long long seed, void* strea
   hipLaunchKernelGGL(bf::bf_fill_random_kernel, dim3(grid), dim3(256), 0, bf::as_stream(stream),
                      static_cast<uint8_t*>(dst), bytes, seed);
   BF_LAUNCHED("bf_fill_random_kernel");
+}
+
+int bf_checksum(const void* src, size_t run_bytes, size_t pitch_bytes, size_t rows, unsigned long long* out,
+                void* stream) {
+  BF_REQUIRE(out != nullptr, "bf_checksum: null output");
+  *out = 0;
+  if (rows == 0 || run_bytes == 0) return BF_OK;
+  BF_REQUIRE(src != nullptr && (reinterpret_cast<uintptr_t>(src) & 3) == 0 && run_bytes % 4 == 0 &&
+                 pitch_bytes % 4 == 0 && (rows == 1 || pitch_bytes >= run_bytes),
+             "bf_checksum: need 4-byte aligned words (run %zu, pitch %zu)", run_bytes, pitch_bytes);
+  hipStream_t st = bf::as_stream(stream);
+  unsigned long long* d = nullptr;
+  BF_HIP(hipMalloc(reinterpret_cast<void**>(&d), sizeof(*d)));
+  hipError_t e = hipMemsetAsync(d, 0, sizeof(*d), st);
+  if (e == hipSuccess) {
+    const size_t words = run_bytes / 4;
+    const unsigned gx = static_cast<unsigned>(std::min<size_t>((words + 255) / 256, 1024));
+    const unsigned gy = static_cast<unsigned>(std::min<size_t>(rows, std::max<size_t>(1, 8192 / gx)));
+    hipLaunchKernelGGL(bf::bf_checksum_kernel, dim3(gx, gy), dim3(256), 0, st, static_cast<const uint32_t*>(src),
+                       words, pitch_bytes / 4, rows, d);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, sizeof(*d), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(d);
+  BF_HIP(e);
+  return BF_OK;
 }
 
 int bf_trace_mark(int tag, void* stream) {

@@ -1,17 +1,14 @@
 // Integer wide fused beamformer: many antennas x beams (config 4: 256 antennas, 64 beams), int8 beams, bit-exact.
-// Two kernels: the 32-beam slab kernel further down (the default, BF_FUSED_PATH_WIDE) and the 16-beam one here
-// (BF_FUSED_PATH_WIDE16, and shapes the 32-beam one does not fit).
+// The 32-beam slab kernels further down are the product (BF_FUSED_PATH_WIDE); the round-1 16-beam slab kernel here is
+// compiled in the diagnostic build only (BF_DIAG: tools/diag_fused.py ablations), as measured slower.
 //
 // Same integer contract as beamform_fused_i8_item_kernel (oracle.fused_beamform_int8: Q14 coefficients of the
 // exact float32 phasors, exact int32 products, one float rounding to int8), organised like the float wide kernel
-// (bf_wide.hip) for a per-item GEMM too large for the item kernel: workgroup = 4 waves x (64 samples, 16 beams,
-// both pols) per (b, c, 16-beam slab); the four slabs of a 64-beam item are XCD-ordered, so slabs after the first
-// re-read the voltages from L2.  The full [[R, I], [-I, R]] Q14 table (the float kernel's [R, -I] + [x_im, -x_re]
-// trick would need -x_re, which overflows int8 at -128) of a 16-beam slab is 2A x 32 x 2 limbs = 32 KiB at A = 256.
-// Per k-step (64 k = 32 antennas) a lane loads 8 antennas' 16-byte runs (uniform base + 32-bit lane offset; the last
-// step is pulled back to [A - 32, A) with zero rows for antennas already covered) and builds each pol's fragment
-// with one v_perm per dword; hi and lo limbs accumulate in separate int32 registers, combined once at the end as
-// (hi << 8) + lo (the item kernel's per-step fold would cost 8 VALU per tile per step here).
+// (bf_wide.hip) for a per-item GEMM too large for the item kernel.  The full [[R, I], [-I, R]] Q14 table (the float
+// kernel's [R, -I] + [x_im, -x_re] trick would need -x_re, which overflows int8 at -128).  Per k-step (64 k = 32
+// antennas) a lane loads 8 antennas' runs (uniform base + 32-bit lane offset; the last step is pulled back to
+// [A - 32, A) with zero rows for antennas already covered) and builds each pol's fragment with one v_perm per dword;
+// hi and lo limbs accumulate in separate int32 registers, combined once at the end as (hi << 8) + lo.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -23,11 +20,13 @@ namespace bf {
 namespace {
 
 constexpr int kW8Threads = 256;
-constexpr int kW8Beams = 16;  // beams per workgroup slab (2 tiles of 16 real columns)
 
 __device__ __forceinline__ int w8_step_base(int s, int A) { return min(32 * s, A - 32); }
 // k-steps of 32 antennas, padded to an even count (ping-pong, see the float wide kernel)
 __host__ __device__ inline int w8_padded_steps(int A) { return 2 * ((((A + 31) >> 5) + 1) / 2); }
+
+#ifdef BF_DIAG  // the 16-beam slab kernel (diagnostic build only)
+constexpr int kW8Beams = 16;  // beams per workgroup slab (2 tiles of 16 real columns)
 
 // The item's voltages as a buffer resource (gfx9 raw-buffer descriptor word 3): every load is then
 // buffer_load_dwordx4 with the lane offset in a VGPR and the wave-uniform antenna offset in an SGPR -- no per-load
@@ -345,6 +344,8 @@ int launch_w8(FusedArgs P, hipStream_t st) {
                        dim3(kW8Threads), lds, st, P);
   BF_LAUNCHED("beamform_fused_i8_wide_kernel");
 }
+
+#endif  // BF_DIAG
 
 // ---- 32-beam slabs (the default integer wide kernel) -------------------------------------------------------------
 // The 16-beam kernel above re-reads each item's voltages once per slab (4x at 64 beams) with a prefetch distance of
@@ -1062,12 +1063,6 @@ int launch_w32(FusedArgs P, hipStream_t st) {
 
 }  // namespace
 
-bool i8_wide_fits(const FusedArgs& P) {
-  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
-  const size_t lds = static_cast<size_t>(w8_padded_steps(P.A)) * 2 * 2 * 64 * 16 + 4 * 32 * 4;
-  return P.A >= 32 && 24 * ant_stride + static_cast<size_t>(P.T) * 4 < (1ull << 32) && lds <= kMaxLds;
-}
-
 bool i8_w32_fits(const FusedArgs& P) {
   const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
   return P.A >= 32 && (P.T & 1) == 0 && 24 * ant_stride + static_cast<size_t>(P.T) * 4 < (1ull << 32) &&
@@ -1075,17 +1070,10 @@ bool i8_w32_fits(const FusedArgs& P) {
 }
 
 template <bool Signed>
-int launch_i8_wide(FusedArgs P, hipStream_t st) {
-  return launch_w8<Signed>(P, st);
-}
-
-template <bool Signed>
 int launch_i8_w32(FusedArgs P, hipStream_t st) {
   return launch_w32<Signed>(P, st);
 }
 
-template int launch_i8_wide<false>(FusedArgs, hipStream_t);
-template int launch_i8_wide<true>(FusedArgs, hipStream_t);
 template int launch_i8_w32<false>(FusedArgs, hipStream_t);
 template int launch_i8_w32<true>(FusedArgs, hipStream_t);
 

@@ -57,6 +57,7 @@ class HostGroup:
         addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = port if port is not None else default_port()
         self.peers = {}
+        self.rejected = []  # rank ids of connections rank 0 dropped (out of range or already registered)
         self.sock = None
         if self.world == 1:
             return
@@ -71,7 +72,16 @@ class HostGroup:
                     conn, _ = srv.accept()
                     conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                     conn.settimeout(op_timeout)  # a rank that never joins a collective fails it, not hangs
-                    (r,) = struct.unpack("!I", _recv_exact(conn, 4))
+                    try:
+                        (r,) = struct.unpack("!I", _recv_exact(conn, 4))
+                    except (OSError, ConnectionError, struct.error):
+                        conn.close()
+                        continue
+                    if not 1 <= r < self.world or r in self.peers:
+                        # a stray connection or a repeated rank id: drop it and keep waiting for the real ranks
+                        self.rejected.append(r)
+                        conn.close()
+                        continue
                     self.peers[r] = conn
             finally:
                 srv.close()

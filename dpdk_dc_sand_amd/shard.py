@@ -57,11 +57,16 @@ def gather_channel_slices(part, group):
 
 class ChannelScatter:
     """The RCCL channel scatter of libbf (bf_comm_* / bf_channel_scatter).  Rank 0 makes the communicator id and
-    `group` (a rendezvous.HostGroup) hands it to every rank; the communicator lives on `context`'s device."""
+    `group` (a rendezvous.HostGroup) hands it to every rank; the communicator lives on `context`'s device.
+
+    bf_comm_create is a blocking RCCL collective, so every rank first checks its local preconditions (the device can
+    be made current, RCCL loads) and the ranks agree over `group` before any of them calls it: a rank that fails
+    early makes every rank raise instead of leaving the others waiting inside ncclCommInitRank."""
 
     def __init__(self, group, context):
         self.group, self.context = group, context
         self.rank, self.world = group.rank, group.world
+        self.handle = None
         uid, err = None, None
         if self.rank == 0:
             buf = ctypes.create_string_buffer(128)
@@ -73,15 +78,46 @@ class ChannelScatter:
         uid = group.broadcast_bytes(uid)
         if not uid:
             raise err or RuntimeError("rank 0 could not create the RCCL communicator id")
-        context.activate()
+        local = None
+        try:
+            context.activate()
+            _lib.call("bf_comm_load")
+        except Exception as e:  # noqa: BLE001 -- reported on every rank below
+            local = e
+        if group.allreduce_any(local is not None):
+            raise local or RuntimeError("RCCL communicator set-up failed on another rank")
         h = ctypes.c_void_p()
         _lib.call("bf_comm_create", ctypes.byref(h), uid, len(uid), self.world, self.rank)
         self.handle = h.value
 
     def scatter(self, band, out, B, A, C, T, queue, root=0):
         """Stream-ordered on `queue`: band (B, A, C*N, T, 2, 2) device array on `root` (None elsewhere) -> `out`
-        (B, A, C, T, 2, 2) device array on every rank."""
+        (B, A, C, T, 2, 2) device array on every rank, written only by RCCL (ncclRecv; the root's own slice by a self
+        send/recv)."""
         _lib.call("bf_channel_scatter", self.handle, _lib.ptr(band), _lib.ptr(out), B, A, C, T, root, queue.handle)
+
+    def stats(self):
+        """(bytes handed to ncclSend, bytes received through ncclRecv) on this rank so far."""
+        s, r = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        _lib.call("bf_comm_stats", self.handle, ctypes.byref(s), ctypes.byref(r))
+        return s.value, r.value
+
+    def verify(self, band, out, B, A, C, T, queue, root=0):
+        """Check every rank's received slice against the root's band without moving either to the host: each rank
+        checksums its slice (bf_checksum), the root checksums each rank's strided region of the band, and the root
+        compares them.  Returns (ok on every rank, [per-rank dict] on the root else None)."""
+        mine = device_checksum(out, C * T * 4 * B * A, 0, 1, queue)
+        got = self.group.gather_json({"rank": self.rank, "checksum": mine})
+        report, ok = None, True
+        if self.rank == root:
+            run = C * T * 4
+            report = []
+            for g in got:
+                want = device_checksum(_lib.ptr(band) + run * g["rank"], run, run * self.world, B * A, queue)
+                report.append({"rank": g["rank"], "checksum": f"{g['checksum']:016x}", "match": g["checksum"] == want})
+            ok = all(r["match"] for r in report)
+        ok = not self.group.allreduce_any(not ok)
+        return ok, report
 
     def allreduce_max(self, value):
         v = ctypes.c_double(float(value))
@@ -98,3 +134,25 @@ class ChannelScatter:
             self.close()
         except Exception:
             pass
+
+
+def device_checksum(src, run_bytes, pitch_bytes, rows, queue):
+    """bf_checksum of a 2-D device region (rows x run_bytes, pitch_bytes apart) on `queue`'s stream."""
+    out = ctypes.c_ulonglong()
+    _lib.call("bf_checksum", _lib.ptr(src), run_bytes, pitch_bytes, rows, ctypes.byref(out), queue.handle)
+    return out.value
+
+
+def host_checksum(words):
+    """CPU restatement of bf_checksum over a packed array of uint32 words (tests)."""
+    w = np.ascontiguousarray(words).reshape(-1).view(np.uint32).astype(np.uint64)
+    i = np.arange(w.size, dtype=np.uint64)
+    return int(np.sum(_splitmix64(_splitmix64(i) ^ w), dtype=np.uint64))
+
+
+def _splitmix64(z):
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))

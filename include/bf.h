@@ -74,7 +74,7 @@ int bf_trace_mark(int tag, void* stream);
  *   delay_vals : f32 (C, M, A, 4) = (delay_s, delay_rate, phase_rad, phase_rate); only [0] and [2] are read
  *   out        : f32 (B, P, C, 2A, 2M), block [[cos, sin], [-sin, cos]] per (a, m), replicated over (b, p)
  * The phase is evaluated in float64 in the reference's operation order, so the output is bit-exact to the
- * oracle. */
+ * oracle.  `out` must be 8-byte aligned (a 16-byte aligned table takes the faster 16-byte-store block form). */
 int bf_coeff_gen(const float* delay_vals, float* out, int B, int P, int C, int Ctot, int A, int M,
                  int xeng_id, double sample_period, void* stream);
 
@@ -129,8 +129,9 @@ int bf_beamform(const uint8_t* x, const float* w, float* y, int B, int P, int C,
 #define BF_FUSED_PATH_ITEM 0x0100    /* one workgroup per (batch, channel) item (A <= 64, T <= 256), else generic */
 #define BF_FUSED_PATH_GENERIC 0x0300 /* any A, any T: groups of 64 antennas */
 #define BF_FUSED_PATH_WIDE 0x0400    /* many antennas x beams: multi-wave beam slabs (config 4) */
-#define BF_FUSED_PATH_WIDE16 0x0500  /* 16-beam slabs (float and int8 wide kernels) */
-/* (0x0200 and 0x0600 named two measured-slower kernels of ABI 1.x, since removed: both are rejected as unknown.) */
+/* (0x0200 and 0x0600 named two measured-slower kernels of ABI 1.x, and 0x0500 (WIDE16) the 16-beam int8 wide kernel
+ * of ABI 2.0, since removed from the product (0x0500: the 16-beam float slabs are what WIDE picks for M <= 16; the
+ * int8 kernel lives on in the diagnostic build): all three are rejected as unknown.) */
 #define BF_FUSED_ORDER_MASK 0x3000
 #define BF_FUSED_ORDER_CHANNEL 0x1000 /* plain channel-fastest workgroup order */
 #define BF_FUSED_ORDER_XCD 0x2000     /* XCD-range order (XCD x streams channels [x C/8, (x+1) C/8)) */
@@ -207,9 +208,14 @@ int bf_pipeline_stage_ms(bf_pipeline* p, long long ticket, float* h2d_ms, float*
  *   bf_comm_unique_id : rank 0 makes the communicator id (BF_COMM_ID_BYTES); the caller hands it to every rank
  *   bf_comm_create    : collective over all ranks, on the device current at the call
  *   bf_channel_scatter: band (B, A, C*N, T, 2, 2) 8-bit on `root` (ignored elsewhere) -> slice (B, A, C, T, 2, 2) on
- *                       every rank; stream-ordered on `stream` (root: per-peer 2-D pack + grouped ncclSend; peers:
- *                       one ncclRecv); the root keeps a staging buffer of (N - 1) slices, grown on demand
- *   bf_comm_allreduce_max: host value -> max over ranks (blocking; timing brackets and agreement checks) */
+ *                       every rank; stream-ordered on `stream` (root: per-rank 2-D pack into a staging buffer of N
+ *                       slices, grown on demand, then one RCCL group of ncclSend per rank plus the root's own
+ *                       ncclRecv -- a self send/recv, so one rank runs the same point-to-point path as N; peers: one
+ *                       ncclRecv).  `slice` is written only by ncclRecv.
+ *   bf_comm_allreduce_max: host value -> max over ranks (blocking; timing brackets and agreement checks)
+ *   bf_comm_stats     : bytes this rank has handed to ncclSend / ncclRecv so far (the scatter's RCCL traffic)
+ *   bf_comm_load      : BF_OK when RCCL can be loaded (a local precondition each rank checks before the collective
+ *                       bf_comm_create, so that no rank waits in it for a rank that already failed) */
 #define BF_COMM_ID_BYTES 128
 typedef struct bf_comm bf_comm;
 int bf_comm_unique_id(void* id, size_t len);
@@ -218,6 +224,14 @@ int bf_comm_destroy(bf_comm* comm);
 int bf_comm_allreduce_max(bf_comm* comm, double* value);
 int bf_channel_scatter(bf_comm* comm, const uint8_t* band, uint8_t* slice, int B, int A, int C, int T, int root,
                        void* stream);
+int bf_comm_stats(const bf_comm* comm, unsigned long long* sent, unsigned long long* received);
+int bf_comm_load(void);
+
+/* Position-weighted 64-bit checksum of a 2-D device region (`rows` runs of `run_bytes`, `pitch_bytes` apart; 4-byte
+ * words): sum over packed word index i of splitmix64(splitmix64(i) ^ word_i), mod 2^64 -- equal for a packed slice
+ * and the strided band region it came from.  Blocking (synchronises `stream`); verification, not the hot path. */
+int bf_checksum(const void* src, size_t run_bytes, size_t pitch_bytes, size_t rows, unsigned long long* out,
+                void* stream);
 
 /* Fill `bytes` of device memory with a deterministic pseudo-random byte stream (splitmix64 of seed and position):
  * synthetic voltages made in HBM (bench.py's full-band cube at N GPUs), no host staging. */

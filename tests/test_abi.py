@@ -99,7 +99,7 @@ def test_pipeline_argument_validation_without_gpu():
 def test_kernel_path_and_contract_flags_are_validated():
     fake = 1 << 20
     args = [fake, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0]
-    for retired in (0x200, 0x600, 0x700):  # 0x200 / 0x600: removed measured-slower kernels (ABI 1.x)
+    for retired in (0x200, 0x500, 0x600, 0x700):  # removed measured-slower kernels (0x500: WIDE16, ABI 2.0)
         with pytest.raises(_lib.BeamformerError, match="unknown kernel path"):
             _lib.call("bf_beamform_fused", *args, retired, 1.0, None)
     with pytest.raises(_lib.BeamformerError, match="unknown workgroup order"):

@@ -137,6 +137,9 @@ def test_bench_rccl_scatter_path_one_rank(tmp_path):
     line = json.loads(lines[0])
     sc = line["scatter"]
     assert sc["backend"] == "rccl" and sc["ranks"] == 1 and "RCCL" in sc["collective"], sc
+    assert line["scatter_ok"] is True and sc["verified"] is True, sc
+    # three timed scatters + nothing else, all through ncclRecv (the self send/recv at one rank)
+    assert sc["rccl_bytes_received_this_rank"] == 3 * sc["bytes_per_rank"], sc
     assert sc["bytes_per_rank"] == 8 * 64 * 4096 * 256 * 4 and sc["seconds"] > 0
     assert line["value"] > 0
 
@@ -148,7 +151,7 @@ def test_channel_scatter_one_rank_comm():
     sys.path.insert(0, ROOT)
     from dpdk_dc_sand_amd import _lib, accel
     from dpdk_dc_sand_amd.rendezvous import HostGroup
-    from dpdk_dc_sand_amd.shard import ChannelScatter
+    from dpdk_dc_sand_amd.shard import ChannelScatter, host_checksum
 
     ctx = accel.create_some_context(device=0)
     q = ctx.create_command_queue()
@@ -164,7 +167,41 @@ def test_channel_scatter_one_rank_comm():
         np.testing.assert_array_equal(again.get(q), host)
         assert len(np.unique(host)) > 200
         out = accel.DeviceArray(ctx, (B, A, C, T, 2, 2), np.uint8)
+        out.set(q, np.zeros((B, A, C, T, 2, 2), np.uint8))
+        assert comm.stats() == (0, 0)
         comm.scatter(band, out, B, A, C, T, q)
         np.testing.assert_array_equal(out.get(q), host)
+        # the slice arrived through RCCL point-to-point: the root packs into staging and its own slice is a self
+        # ncclSend/ncclRecv (bf_channel_scatter writes `slice` only through ncclRecv)
+        assert comm.stats() == (host.nbytes, host.nbytes)
+        ok, per_rank = comm.verify(band, out, B, A, C, T, q)
+        assert ok and per_rank == [{"rank": 0, "checksum": f"{host_checksum(host):016x}", "match": True}]
+        # a slice that differs from the band by one byte fails the check
+        bad = host.copy()
+        bad[1, 2, 3, 4, 1, 0] ^= 1
+        out.set(q, bad)
+        ok, per_rank = comm.verify(band, out, B, A, C, T, q)
+        assert not ok and not per_rank[0]["match"]
     finally:
         comm.close()
+
+
+def test_device_checksum_matches_restatement():
+    """bf_checksum == shard.host_checksum, contiguous and for a strided (band, rank) region == the packed slice."""
+    sys.path.insert(0, ROOT)
+    from dpdk_dc_sand_amd import _lib, accel
+    from dpdk_dc_sand_amd.shard import device_checksum, host_checksum, pack_channel_slices
+
+    ctx = accel.create_some_context(device=0)
+    q = ctx.create_command_queue()
+    B, A, N, C, T = 3, 5, 4, 6, 48
+    band = accel.DeviceArray(ctx, (B, A, N * C, T, 2, 2), np.uint8)
+    _lib.call("bf_fill_random", band.ptr, band.nbytes, 11, q.handle)
+    host = band.get(q)
+    assert device_checksum(band, host.nbytes, 0, 1, q) == host_checksum(host)
+    run = C * T * 4
+    for r, part in enumerate(pack_channel_slices(host, N)):
+        assert device_checksum(band.ptr + r * run, run, run * N, B * A, q) == host_checksum(part)
+    big = accel.DeviceArray(ctx, (1 << 26,), np.uint8)  # 64 MiB: many workgroups, one atomic per wave
+    _lib.call("bf_fill_random", big.ptr, big.nbytes, 3, q.handle)
+    assert device_checksum(big, big.nbytes, 0, 1, q) == host_checksum(big.get(q))

@@ -146,6 +146,24 @@ def test_coeff_gen_tiled_matches_oracle(context, command_queue, A, M, C):
     np.testing.assert_array_equal(O.coeffs(d, 2, 2, C, 8192, A, M, 3), w)
 
 
+@pytest.mark.parametrize("A,M", [(5, 3), (64, 16)])
+def test_coeff_gen_8_byte_aligned_output(context, command_queue, A, M):
+    """bf_coeff_gen requires an 8-byte aligned table: at an address that is 8 but not 16-byte aligned (a C-ABI
+    caller's offset pointer) it must not take the 16-byte-store block form, and the table is the contract's."""
+    B, P, C, Ctot = 2, 2, 3, 4096
+    d = random_delays(C, M, A, 5 * A + M)
+    dv = accel.DeviceArray(context, d.shape, np.float32)
+    dv.set(command_queue, d)
+    n = B * P * C * 2 * A * 2 * M
+    buf = accel.DeviceArray(context, (n + 4,), np.float32)
+    buf.set(command_queue, np.full(n + 4, 7.0, np.float32))
+    _lib.call("bf_coeff_gen", dv.ptr, buf.ptr + 8, B, P, C, Ctot, A, M, 1, TS, command_queue.handle)
+    got = buf.get(command_queue)
+    np.testing.assert_array_equal(got[2:2 + n].reshape(B, P, C, 2 * A, 2 * M), O.coeffs(d, B, P, C, Ctot, A, M, 1))
+    np.testing.assert_array_equal(got[:2], [7.0, 7.0])
+    np.testing.assert_array_equal(got[2 + n:], [7.0, 7.0])
+
+
 def test_coeff_gen_time_matches_oracle(context, command_queue):
     from dpdk_dc_sand_amd import accel
     C, A, M, Ctot, nt = 6, 5, 3, 4096, 4
@@ -348,7 +366,7 @@ def test_fused_equals_op_sequence_bitwise(context, command_queue, fused_path):
                           O.coeffs(d, B, 2, C, Ctot, A, M, 2))
 
 
-@pytest.fixture(params=["auto", "item", "generic", "wide", "wide16"])
+@pytest.fixture(params=["auto", "item", "generic", "wide"])
 def fused_path(request):
     """Run a fused test through each kernel (FusedBeamformerTemplate kernel_path = BF_FUSED_PATH_* flags): the
     automatic choice, the single-item kernel (A <= 64, T <= 256), the generic kernel, and the wide kernel (many antennas x beams) with 32- and 16-beam slabs.  A path that does not fit a shape
@@ -384,8 +402,8 @@ def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C
     (19, 3, 7, 48, 2, 7, False), (130, 9, 2, 64, 2, 1, True), (256, 64, 1, 32, 1, 1, False),
     (4, 1, 16, 1024, 1, 16, True), (80, 24, 3, 16, 3, 1, True), (32, 8, 4, 64, 2, 1, False),
     (48, 12, 2, 128, 2, 1, False), (33, 5, 3, 80, 2, 3, True), (16, 8, 3, 48, 2, 1, True),
-    (64, 16, 2, 112, 1, 1, False), (40, 32, 2, 64, 1, 2, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel", "wide16"])
+    (64, 16, 2, 112, 1, 1, False), (40, 32, 2, 64, 1, 2, True), (600, 5, 1, 32, 1, 1, True)])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel"])
 def test_fused_int8_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """int8 (requantised) beams: the integer MFMA path reproduces the oracle's integer contract bit for bit, on the
     item kernel (A <= 64, T <= 256; others fall through to generic) and the generic kernel (any A, T)."""
@@ -404,6 +422,37 @@ def test_fused_int8_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, 
         assert q.dtype == np.int8
         np.testing.assert_array_equal(q, ref)
         assert np.abs(ref.astype(int)).max() >= 4  # not a trivially zero case
+
+
+@pytest.mark.parametrize("A,M,C,T", [(64, 16, 4, 256), (256, 64, 8, 256), (19, 3, 5, 48)])
+@pytest.mark.parametrize("signed", [True, False])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel", "f32"])
+def test_fused_int8_requant_double_rounding(context, command_queue, i8_kernel, A, M, C, T, signed):
+    """The requantisation's two roundings, RN(float32(y) * s) and then rne, at a scale that is not a power of two.
+    Zero delays and phases make every Q14 coefficient (16384, 0), and only antenna 0 carries voltages, so
+    y = 16384 x and the requantiser sees x * scale: at scale = float32(1/6) that product rounds onto a half-integer
+    for 22 of the 256 byte values x, where one fused multiply-add (a single rounding) would give the other integer.
+    Every int8 path must give the contract's value (oracle.fused_beamform_int8; oracle.requantise of the float beams
+    for the float path)."""
+    Ctot, scale = 4096, float(np.float32(1 / 6))
+    rng = np.random.default_rng(A + T)
+    raw = np.zeros((1, A, C, T, 2, 2), np.uint8)
+    raw[:, 0] = rng.integers(0, 256, (1, C, T, 2, 2), dtype=np.uint8)
+    if signed:
+        raw = raw.view(np.int8)
+    d = np.zeros((1, M, A, 4), np.float32)
+    ref = O.fused_beamform_int8(raw, d, Ctot, scale=scale, signed=signed)
+    # the test has teeth: a single-rounding requantiser differs from the contract on this input
+    y = 16384.0 * (raw[0, 0].view(np.int8) if signed else raw[0, 0]).astype(np.float64)
+    s = np.float32(np.float32(scale) * np.float32(2.0 ** -14))
+    once = np.clip(np.rint(y.astype(np.float32).astype(np.float64) * np.float64(s)), -127, 127)
+    twice = np.clip(np.rint(y.astype(np.float32) * s), -127, 127)
+    assert np.count_nonzero(once != twice) > 0
+    kw = dict(int8_contract="f32") if i8_kernel == "f32" else i8_path(i8_kernel)
+    op = FusedBeamformerTemplate(context, 1, C, Ctot, T, A, M, delay_channels=1, sample_signed=signed, out_int8=True,
+                                 out_scale=scale, **kw).instantiate(command_queue)
+    (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    np.testing.assert_array_equal(q, ref)
 
 
 @pytest.mark.parametrize("M", [1, 2])
@@ -522,7 +571,7 @@ def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, 
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
     (64, 16, 3, 256, 2, 1, True), (64, 16, 2, 256, 2, 1, False), (19, 3, 4, 48, 2, 4, False),
     (130, 9, 2, 64, 1, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel", "wide16"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel"])
 def test_fused_int8_beam_weights_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """Weighted int8 beams: Q14 limbs of the weighted float32 coefficients, bit-exact to the integer contract."""
     Ctot, xeng, t0, bdt = 4096, 2, 1e-3, 256 * 8192 * TS
@@ -561,7 +610,7 @@ def boundary_delays(M, A, seed):
 
 @pytest.mark.parametrize("A,M,C,T,B,signed", [(64, 16, 3, 256, 2, True), (64, 16, 2, 256, 2, False),
                                               (19, 3, 3, 48, 2, False), (256, 64, 1, 32, 1, True)])
-@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel", "wide16"])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel"])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_fused_int8_rounding_boundaries(context, command_queue, i8_kernel, weighted, A, M, C, T, B,
                                         signed):

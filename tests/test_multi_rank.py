@@ -137,3 +137,73 @@ def test_comm_argument_validation_without_gpu():
     with pytest.raises(_lib.BeamformerError, match="null pointer"):
         _lib.call("bf_channel_scatter", None, None, None, 1, 1, 1, 16, 0, None)
     assert _lib.load().bf_comm_destroy(None) == 0
+
+
+def _stray_worker(rank, world, port, q):
+    """Rank 0 of a world-2 group; before rank 1 connects, two strays do: one claiming rank 7 (out of range) and one
+    claiming rank 0 (the root's own id).  Both must be dropped and the real rank 1 accepted."""
+    import struct
+    import time
+    from dpdk_dc_sand_amd.rendezvous import HostGroup
+    try:
+        if rank == 0:
+            g = HostGroup(0, world, "127.0.0.1", port)
+            v = g.allreduce_max(1.0)
+            rejected = list(g.rejected)
+            g.close()
+            q.put((rank, "ok", v, rejected))
+        else:
+            strays = []
+            for bad in (7, 0):
+                deadline = time.monotonic() + 60
+                while True:
+                    try:
+                        s = socket.create_connection(("127.0.0.1", port), timeout=5.0)
+                        break
+                    except OSError:
+                        if time.monotonic() > deadline:
+                            raise
+                        time.sleep(0.05)
+                s.sendall(struct.pack("!I", bad))
+                strays.append(s)
+            time.sleep(0.5)
+            g = HostGroup(1, world, "127.0.0.1", port)
+            v = g.allreduce_max(2.0)
+            g.close()
+            for s in strays:
+                s.close()
+            q.put((rank, "ok", v, None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, "error " + repr(e), None, None))
+
+
+def test_rendezvous_rejects_stray_and_duplicate_rank_ids():
+    res = _run_world(_stray_worker, 2)
+    assert all(r[1] == "ok" for r in res), res
+    assert res[0][2] == res[1][2] == 2.0
+    assert sorted(res[0][3]) == [0, 7]
+
+
+def test_host_checksum_restatement():
+    """The CPU restatement of bf_checksum (shard.host_checksum, what the GPU kernel is tested against): position
+    sensitive, and the strided band region of a rank equals its packed slice."""
+    from dpdk_dc_sand_amd.shard import host_checksum
+    rng = np.random.default_rng(2)
+    band = rng.integers(0, 256, (2, 3, 4 * 8, 16, 2, 2), dtype=np.uint8)
+    parts = pack_channel_slices(band, 4)
+    sums = [host_checksum(p) for p in parts]
+    assert len(set(sums)) == 4
+    w = parts[1].reshape(-1).view(np.uint32).copy()
+    w[[3, 5]] = w[[5, 3]]
+    assert w[3] == w[5] or host_checksum(w) != sums[1]
+    assert host_checksum(np.zeros(0, np.uint32)) == 0
+
+
+def test_checksum_and_comm_stats_argument_validation_without_gpu():
+    out = ctypes.c_ulonglong(5)
+    with pytest.raises(_lib.BeamformerError, match="4-byte"):
+        _lib.call("bf_checksum", 1 << 20, 6, 8, 2, ctypes.byref(out), None)
+    assert out.value == 0
+    _lib.call("bf_checksum", 1 << 20, 0, 0, 3, ctypes.byref(out), None)  # empty region: 0, no device touched
+    with pytest.raises(_lib.BeamformerError, match="null pointer"):
+        _lib.call("bf_comm_stats", None, ctypes.byref(out), ctypes.byref(out))
