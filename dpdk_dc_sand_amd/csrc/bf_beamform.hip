@@ -540,8 +540,8 @@ __global__ __launch_bounds__(kThreads, 2) void beamform_table_persist_kernel(
 constexpr int kOsCols = 128, kOsRows = 256;
 constexpr size_t kOsLds = 2 * 2 * 8 * 2 * 64 * 16;  // 2 buffers x 2 steps x 8 tiles x 2 limbs x 64 lanes x 16 B
 
-template <bool Signed, int Mode, int NW>
-__global__ __launch_bounds__(NW * 64, NW / 2) void beamform_table_os_kernel(const uint8_t* __restrict__ x,
+template <bool Signed, int Mode, int NW, int Occ = NW / 2>
+__global__ __launch_bounds__(NW * 64, Occ) void beamform_table_os_kernel(const uint8_t* __restrict__ x,
                                                                       const float* __restrict__ w,
                                                                       float* __restrict__ y, int A) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
@@ -685,10 +685,10 @@ inline bool table_os_fits(int NB, int A, int M, const uint8_t* x, const float* w
          (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0;
 }
 
-template <bool Signed, int Mode = 0, int NW = 8>
+template <bool Signed, int Mode = 0, int NW = 8, int Occ = NW / 2>
 int launch_table_os(const uint8_t* x, const float* w, float* y, long long bpc, int A, hipStream_t st) {
   BF_REQUIRE(bpc < (1LL << 31), "bf_beamform: grid too large");
-  hipLaunchKernelGGL((beamform_table_os_kernel<Signed, Mode, NW>), dim3(static_cast<unsigned>(bpc)), dim3(NW * 64),
+  hipLaunchKernelGGL((beamform_table_os_kernel<Signed, Mode, NW, Occ>), dim3(static_cast<unsigned>(bpc)), dim3(NW * 64),
                      kOsLds, st, x, w, y, A);
   BF_LAUNCHED("beamform_table_os_kernel");
 }
@@ -853,6 +853,7 @@ extern "C" int bf_diag_table(int mode, int nts, const uint8_t* x, const float* w
     case 416: return bf::launch_table_os<true, 16, 8>(x, w, y, bpc, A, st);
     case 428: return bf::launch_table_os<true, 28, 8>(x, w, y, bpc, A, st);
     case 500: return bf::launch_table_os<true, 0, 4>(x, w, y, bpc, A, st);
+    case 600: return bf::launch_table_os<true, 0, 8, 3>(x, w, y, bpc, A, st);  // 8 waves, <= 168 VGPRs, 1 WG/CU
     case 528: return bf::launch_table_os<true, 28, 4>(x, w, y, bpc, A, st);
     // four row groups per pass (each LDS coefficient fragment feeds 8 MFMAs instead of 4), ring depth 8
     case 240: return bf::launch_persist<true, 2, 8, 8, 0, 4>(x, w, y, bpc, NB, A, M, S, NT, st);

@@ -154,6 +154,13 @@ __device__ __forceinline__ int q14_pair_unit(double v, bool* ok) {
   return q14_pair(v, 16384.0f, ok);
 }
 
+// q14_pair_unit on t = 2^14 v given directly (a recurrence kept in the 2^14-scaled domain: no rescale per value).
+__device__ __forceinline__ int q14_pair_unit_scaled(double t, bool* ok) {
+  const double n = rint(t);
+  if (fabs(t - n) < kQ14UnitMargin) return static_cast<int>(n);
+  return q14_pair(t * 0x1p-14, 16384.0f, ok);
+}
+
 // The truncated fdlibm coefficients (cos C5..C1, -1/2; sin S5..S1) as device memory, not literals: loaded once into
 // SGRPs by s_load, each Horner step is then one VOP3 v_fma_f64 with an SGPR operand, where literal constants made
 // the compiler rematerialise every addend with two v_mov_b32 per step (21 of ~96 VALU per phasor).

@@ -107,21 +107,25 @@ __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
   const float mag = fabsf(static_cast<float>(tau)) * static_cast<float>((ch_last + half) * fabs(P.k)) +
                     fabsf(static_cast<float>(phi));
   const bool in_range = mag < kQ14MaxMag;
-  double re = 1.0, im = 0.0, cd = 1.0, sd = 0.0;
+  // The recurrence runs on 2^14 x the phasor (a power-of-two scale commutes with every rounding, so each value is
+  // exactly 2^14 times the unscaled recurrence's): the unit-gain decision then starts from t = 2^14 v itself.
+  double re = 16384.0, im = 0.0, cd = 1.0, sd = 0.0;
   if (in_range) {
     const double ch0 = static_cast<double>(P.base_ch + c0);
     sincos_pio2(fma(tau * (ch0 - half), P.k, phi), &im, &re);  // the anchor: rot(c0), as q14_fast forms it
     sincos_pio2(tau * P.k, &sd, &cd);                          // one channel's rotation
+    re *= 16384.0;
+    im *= 16384.0;
   }
   for (int j = 0; j < nrun; ++j) {
     bool ok = in_range;
     int wc, ws;
     if (Gain || !P.unit_fast) {  // (uniform)
-      wc = q14_pair(re, gq, &ok);
-      ws = q14_pair(im, gq, &ok);
+      wc = q14_pair(re * 0x1p-14, gq, &ok);
+      ws = q14_pair(im * 0x1p-14, gq, &ok);
     } else {
-      wc = q14_pair_unit(re, &ok);
-      ws = q14_pair_unit(im, &ok);
+      wc = q14_pair_unit_scaled(re, &ok);
+      ws = q14_pair_unit_scaled(im, &ok);
     }
     if (!ok) q14_exact(d, static_cast<double>(P.base_ch + c0 + j), P.ctot, P.ts, dt, P.gain, g, &wc, &ws);
     o[static_cast<size_t>(j) * words] = (static_cast<uint32_t>(wc) & 0xffffu) | (static_cast<uint32_t>(ws) << 16);

@@ -416,6 +416,23 @@ __device__ __forceinline__ void w32_load(const uint8_t* __restrict__ base, size_
   }
 }
 
+// The same loads through a buffer resource on the workgroup's (b, c0) block: every load is buffer_load_dwordx2 with
+// the lane part of the offset in one VGPR (antenna group 8h of the step, the sample pair) and the wave-uniform part
+// -- row (a0 + q) of the step, the channel -- in an SGPR soffset: no per-load 64-bit address arithmetic on the VALU
+// (the pointer form spends a v_mad_u64_u32 and moves per load).  Offsets below 2^31 (the host checks A C T 4).
+template <int Mode>
+__device__ __forceinline__ void w32_load_buf(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t sbase, uint32_t stride,
+                                             u32x2_t (&d)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if constexpr (Mode & 8) {
+      d[q] = u32x2_t{voff * 0x01010101u + sbase + q, voff * 0x01010101u + sbase - q};
+      continue;
+    }
+    d[q] = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, sbase + q * stride, 0));
+  }
+}
+
 // The step's B fragments [pol][sample] (one v_perm per dword); the voltage registers are free afterwards.
 template <bool Signed>
 __device__ __forceinline__ void w32_frags(const u32x2_t (&d)[8], i32x4_t (&f)[2][2]) {
@@ -765,7 +782,10 @@ constexpr int kW32TChannels = 4;
 // 16 steps are straight-line code: the four step buffers keep their registers, and the compiler no longer re-homes
 // them through copies behind s_waitcnt vmcnt(22 .. 0) at every loop header -- a full drain of the voltage prefetch
 // every four steps in the runtime-bounded form.
-template <bool Signed, int Mode = 0, bool Early = true, int kSp = 0, int kNP = 0, int kNB = 4, int kCh = kW32TChannels>
+// BufLd: voltage loads through a buffer resource (w32_load_buf).  Pow2: the output scale is a power of two, so the
+// requantisation's multiply and magic add fuse into one exact FMA (requant_bits<true>).
+template <bool Signed, int Mode = 0, bool Early = true, int kSp = 0, int kNP = 0, int kNB = 4, int kCh = kW32TChannels,
+          bool BufLd = false, bool Pow2 = false>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -803,10 +823,19 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
   __builtin_assume(Sp >= 4 && (Sp & 3) == 0 && npasses >= 1 && nk >= 1);
   const int total = nk * npasses * Sp;
   int issued = 0, ls = 0, lp = 0, lk = 0;
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7fffffff,
+                                                                        0x00020000);
   auto issue = [&](u32x2_t (&d)[8]) {
-    const uint32_t loff = hoff + static_cast<uint32_t>(lk) * ch_bytes +
-                          static_cast<uint32_t>(min((wave + 4 * lp) * 16 + tl, T2 - 1)) * 8u;
-    w32_load<Mode>(base, ant_stride, loff, ls, P.A, d);
+    if constexpr (BufLd) {
+      const uint32_t voff = hoff + static_cast<uint32_t>(min((wave + 4 * lp) * 16 + tl, T2 - 1)) * 8u;
+      const uint32_t sbase = static_cast<uint32_t>(w8_step_base(ls, P.A)) * static_cast<uint32_t>(ant_stride) +
+                             static_cast<uint32_t>(lk) * ch_bytes;
+      w32_load_buf<Mode>(vrs, voff, sbase, static_cast<uint32_t>(ant_stride), d);
+    } else {
+      const uint32_t loff = hoff + static_cast<uint32_t>(lk) * ch_bytes +
+                            static_cast<uint32_t>(min((wave + 4 * lp) * 16 + tl, T2 - 1)) * 8u;
+      w32_load<Mode>(base, ant_stride, loff, ls, P.A, d);
+    }
     ++issued;  // selects, not branches (see the one-channel kernel); past the last step it repeats that step
     const bool adv = issued < total;
     const bool wrap = ls + 1 == Sp, pwrap = lp + 1 == npasses;
@@ -831,7 +860,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
   };
   load_table(0);
   __builtin_amdgcn_sched_barrier(0);
-  constexpr int NB = kSp ? kNB : 4;  // step buffers (NB - 1 steps in flight while one is contracted)
+  constexpr int NB = kSp ? kNB : 2;  // step buffers (NB - 1 steps in flight while one is contracted)
   u32x2_t db[NB][8];
 #pragma unroll
   for (int j = 0; j < NB; ++j) issue(db[j]);
@@ -902,10 +931,12 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
-        for (int s = 0; s < Sp; s += 4) {
+        // runtime step count (Sp a multiple of 4): the two-buffer ring, a pair of steps per iteration, so every
+        // channel's steps start at buffer 0
+        for (int s = 0; s < Sp; s += 2) {
           i32x4_t f[2][2];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < 2; ++j) {
             w32_frags<Signed>(db[j], f);
             issue(db[j]);
             w32_mfma<0>(lds4, s + j, lane, f, hi, lo);
@@ -949,7 +980,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
               for (int r = 0; r < 4; ++r) {
                 int y = (hi[p][i][t][r] << 8) + lo[p][i][t][r];
                 if constexpr (!Signed) y += 128 * csr[r];
-                qb[r] = requant_bits(y, s32);
+                qb[r] = requant_bits<Pow2>(y, s32);
               }
               pk[i][t] = pack_low_bytes(qb[0], qb[1], qb[2], qb[3]);
             }
@@ -981,12 +1012,20 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
       }
     };
     if constexpr (Early) {
+      if constexpr (kNP != 0) {
 #pragma unroll
-      for (int pass = 0; pass + 1 < npasses; ++pass) run_pass(pass, std::false_type{});
+        for (int pass = 0; pass + 1 < kNP; ++pass) run_pass(pass, std::false_type{});
+      } else {
+        for (int pass = 0; pass + 1 < npasses; ++pass) run_pass(pass, std::false_type{});
+      }
       run_pass(npasses - 1, std::true_type{});
     } else {
+      if constexpr (kNP != 0) {
 #pragma unroll
-      for (int pass = 0; pass < npasses; ++pass) run_pass(pass, std::false_type{});
+        for (int pass = 0; pass < kNP; ++pass) run_pass(pass, std::false_type{});
+      } else {
+        for (int pass = 0; pass < npasses; ++pass) run_pass(pass, std::false_type{});
+      }
       load_table(min(kc + 1, nk - 1));
     }
     if constexpr (kSp != 0 && (kSp * kNP) % NB != 0) {  // re-align the ring: the next channel starts at buffer 0
@@ -1042,14 +1081,24 @@ int launch_w32(FusedArgs P, hipStream_t st) {
     const int ch = straight ? 8 : kW32TChannels;
     const long long groups = static_cast<long long>(P.B) * ((Cn + ch - 1) / ch);
     const long long tgrid = P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs;
+    // buffer-resource voltage loads (no per-load VALU addressing) while every in-workgroup offset is below 2^31
+    const bool buf = static_cast<unsigned long long>(P.A) * P.C * P.T * 4 < (1ull << 31);
+    // a power-of-two scale: the requantisation's multiply and magic add as one exact FMA
+    const bool pow2 = scale_is_pow2(P.out_scale * 0x1p-14f);
+    const dim3 grid3(static_cast<unsigned>(tgrid)), block(kW8Threads);
     // config 4's shape: the straight-line ring, two step buffers (one step in flight while one is contracted):
     // 377 vs 384 us for three buffers and 403 for the runtime loop (profiles/r3_ab_*, r3_g_*)
-    if (straight)
-      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false, 8, 2, 2, 8>),
-                         dim3(static_cast<unsigned>(tgrid)), dim3(kW8Threads), lds, st, P);
-    else
-      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false>), dim3(static_cast<unsigned>(tgrid)),
-                         dim3(kW8Threads), lds, st, P);
+    if (straight && buf && pow2)
+      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false, 8, 2, 2, 8, true, true>), grid3, block,
+                         lds, st, P);
+    else if (straight && buf)
+      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false, 8, 2, 2, 8, true, false>), grid3, block,
+                         lds, st, P);
+    else if (buf)
+      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false, 0, 0, 4, kW32TChannels, true, false>),
+                         grid3, block, lds, st, P);
+    else  // offsets past 2^31 (A C T 4 >= 2 GiB): the pointer form
+      hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false>), grid3, block, lds, st, P);
     BF_LAUNCHED("beamform_fused_i8_w32t_kernel");
   }
   if (P.gain)
@@ -1144,10 +1193,16 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   case 260 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 16>), dim3(grid_for(16)), dim3(bf::kW8Threads), lds, st, P); break; \
   case 280 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, true, 8, 2, 2, 8>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
   case 500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, true, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break
+#define BF_W32TB(m) \
+  case 900 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8, true, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 920 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 3, 8, true, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
+  case 940 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8, false, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break
   switch (mode) {
     BF_W32T(0); BF_W32T(1); BF_W32T(4); BF_W32T(8); BF_W32T(9); BF_W32T(12);
+    BF_W32TB(0); BF_W32TB(1); BF_W32TB(4); BF_W32TB(8); BF_W32TB(9); BF_W32TB(12);
     default: return BF_ERR_ARG;
   }
+#undef BF_W32TB
 #undef BF_W32T
   BF_LAUNCHED("beamform_fused_i8_w32t_kernel");
 }

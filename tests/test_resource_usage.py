@@ -1,0 +1,64 @@
+"""Build hygiene of the product kernels (no GPU): every kernel instance libbf.so contains compiles for gfx950 with no
+scratch (register spills) and without failed unroll requests.  Runs hipcc on the product sources (device code only,
+the Makefile's flags) with -Rpass-analysis=kernel-resource-usage, as tools/resource_usage.py does; the diagnostic
+build (BF_DIAG) is not checked."""
+import os
+import re
+import shutil
+import subprocess
+from concurrent.futures import ThreadPoolExecutor
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "dpdk_dc_sand_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+SOURCES = ["bf_coeff.hip", "bf_reorder.hip", "bf_beamform.hip", "bf_fused.hip", "bf_wide.hip", "bf_wide_i8.hip",
+           "bf_q14table.hip", "bf_requant.hip", "bf_wide_i8os.hip"]
+
+
+def _usage(src):
+    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
+           "-x", "hip", "--cuda-device-only", "-c", os.path.join(CSRC, src), "-o", os.devnull,
+           "-Rpass-analysis=kernel-resource-usage"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    kernels, cur = [], None
+    for line in r.stderr.splitlines():
+        m = re.search(r"remark: (.*?) \[-Rpass", line)
+        if not m:
+            continue
+        t = m.group(1).strip()
+        if t.startswith("Function Name:"):
+            cur = {"name": t.split(":", 1)[1].strip()}
+            kernels.append(cur)
+        elif cur is not None and ":" in t:
+            k, v = t.split(":", 1)
+            cur[k.strip()] = v.strip()
+    warnings = [ln for ln in r.stderr.splitlines() if "warning:" in ln]
+    return src, kernels, warnings
+
+
+@pytest.fixture(scope="module")
+def usage():
+    if not os.path.exists(HIPCC) or shutil.which("c++filt") is None:
+        pytest.skip("hipcc not available")
+    with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        return {src: (k, w) for src, k, w in ex.map(_usage, SOURCES)}
+
+
+def test_no_scratch_in_any_product_kernel(usage):
+    spills = []
+    for src, (kernels, _) in usage.items():
+        assert kernels or src == "bf_wide_i8os.hip", f"no kernels reported for {src}"
+        for k in kernels:
+            if int(k.get("ScratchSize [bytes/lane]", "0")) != 0:
+                name = subprocess.run(["c++filt"], input=k["name"], capture_output=True, text=True).stdout.strip()
+                spills.append(f"{src}: {name[:120]} scratch {k['ScratchSize [bytes/lane]']} B/lane, "
+                              f"VGPRs {k.get('VGPRs')}")
+    assert not spills, "\n".join(spills)
+
+
+def test_no_compiler_warnings_in_product_sources(usage):
+    warnings = [w for _, (_, ws) in usage.items() for w in ws]
+    assert not warnings, "\n".join(warnings[:20])

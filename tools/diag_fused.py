@@ -89,6 +89,10 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
     tnames.update({220: "full [NB2, 2 ch/WG]", 240: "full [NB2, 8 ch/WG]", 260: "full [NB2, 16 ch/WG]",
                    280: "full [NB2, 8 ch/WG, early table]"})
     tnames.update({500 + m: v + " [unrolled NB3, early table]" for m, v in base.items()})
+    # round 4: buffer-resource voltage loads (SGPR row offsets, no per-load VALU addressing) + power-of-two FMA requant
+    tnames.update({900 + m: v.replace("early ", "") + " [NB2, 8 ch, buffer loads]" for m, v in base.items()})
+    tnames.update({920 + m: v.replace("early ", "") + " [NB3, 8 ch, buffer loads]" for m, v in base.items()})
+    tnames.update({940 + m: v.replace("early ", "") + " [NB2, 8 ch, pointer loads, pow2]" for m, v in base.items()})
     # 700 + m: the output-stationary LDS-DMA kernel (bf_wide_i8os.hip) on the same table; m = its Mode bits
     tnames.update({700 + m: v.replace("early ", "") + " [os, LDS-DMA]" for m, v in base.items() if m in (0, 1, 4, 8, 9, 12)})
     tnames.update({702: "no-mfma [os]", 705: "no table,no-store [os]",
@@ -108,7 +112,7 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
                                      1 / 1712e6, q.handle)
     for mode in tnames:
         assert mode < 0 or w32t_call(mode, 0) == 0, mode
-    for alt in (220, 240, 260, 280, 700):  # another kernel form's int8 beams on the same input and table: bitwise equal
+    for alt in (220, 240, 260, 280, 700, 900, 920, 940):  # another form's int8 beams, same input and table: bitwise equal
         if alt not in tnames:
             continue
         outs = []
@@ -263,7 +267,7 @@ if "table" in _os.environ.get("DIAG_KERNELS", ""):  # the MatrixMultiply drop-in
                    240: "persistent G4 R8", 268: "persistent G4 R8, only MFMA+staging", 250: "persistent G4 R16",
                    278: "persistent G4 R16, only MFMA+staging", 400: "output-stationary", 404: "os, no stores",
                    408: "os, no x loads", 416: "os, no table loads", 428: "os, only MFMA+staging",
-                   500: "os 4 waves", 528: "os 4 waves, only MFMA+staging"})
+                   500: "os 4 waves", 528: "os 4 waves, only MFMA+staging", 600: "os 8 waves, occupancy 3 (no spill)"})
     if _os.environ.get("TABLE_MODES"):  # e.g. 0,100: interleaved A/B over DIAG_ROUNDS, medians
         tnames = {int(m): tnames.get(int(m), str(m)) for m in _os.environ["TABLE_MODES"].split(",")}
     for nts in [int(v) for v in _os.environ.get("TABLE_NTS", "2,4").split(",")]:
