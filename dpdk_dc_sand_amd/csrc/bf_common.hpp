@@ -87,4 +87,14 @@ inline bool q14_sum_bound_ok(int A, bool sample_signed, double max_gain) {
 // Compute units of the current device (cached per device index; sizes persistent grids only).
 int cu_count();
 
+// A second stream on the current device for work a call forks off its caller's stream and joins back (the int8
+// wide path's coefficient generator running beside the contraction), and a pool of events for the hand-offs.
+// Thread-local per device: concurrent callers on other host threads never serialise on one another's helper.
+// Returns nullptr (and sets the error) if the stream or events cannot be created.
+struct AuxStream {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[17] = {};  // [0] fork, [1 + k] chunk k done
+};
+AuxStream* aux_stream();
+
 }  // namespace bf

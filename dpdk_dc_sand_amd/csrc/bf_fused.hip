@@ -644,7 +644,7 @@ __global__ __launch_bounds__(kThreads) void beamform_fused_i8_kernel(FusedArgs P
 
 // Requantise 4 int32 beam components (columns cl0..cl0+3 of the slab) to packed int8: the integer contract
 // q = clamp(rne(f32(y) * f32(scale * 2^-14)), +-127); unsigned input adds back 128 * column sum (4 wave partials).
-template <bool Signed>
+template <bool Signed, bool Pow2 = false>
 __device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* colsum, int cl0, float s32) {
   uint32_t q[4];
 #pragma unroll
@@ -654,7 +654,7 @@ __device__ __forceinline__ uint32_t requant4(const i32x4_t& acc, const int* cols
       const int cl = cl0 + r;
       y += 128 * (colsum[cl] + colsum[32 + cl] + colsum[64 + cl] + colsum[96 + cl]);
     }
-    q[r] = requant_bits(y, s32);
+    q[r] = requant_bits<Pow2>(y, s32);
   }
   return pack_low_bytes(q[0], q[1], q[2], q[3]);
 }
@@ -747,7 +747,7 @@ __device__ __forceinline__ void i8_coef_phase(int8_t* lb, int* colsum, const Coe
 
 // Full-slab contraction: sample row i outermost, both pols inside, each 4-MFMA chain (hi limbs, << 8, lo limbs)
 // requantised at once into packed int8 columns pkall[p][tau][i] (lane (tl, h): row 4 tq + i, columns 16 tau + 4 h ..).
-template <bool Signed, int NTS>
+template <bool Signed, int NTS, bool Pow2 = false>
 __device__ __forceinline__ void i8_contract_rows(const int4* fr, const uint32_t (&d)[2][8][4], const int* colsum,
                                                  float s32, int S8, int lane, int h, uint32_t (&pkall)[2][NTS][4]) {
   i32x4_t chi[2][NTS], clo[2][NTS];
@@ -792,7 +792,7 @@ __device__ __forceinline__ void i8_contract_rows(const int4* fr, const uint32_t 
         t = t << 8;
         t = mfma_i8(clo[0][tau], f[0], t);
         t = mfma_i8(clo[1][tau], f[1], t);
-        pkall[p][tau][i] = requant4<Signed>(t, colsum, 16 * tau + 4 * h, s32);
+        pkall[p][tau][i] = requant4<Signed, Pow2>(t, colsum, 16 * tau + 4 * h, s32);
       }
     }
   }
@@ -873,7 +873,8 @@ __device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, in
 // (f32 sincos) coefficients only (inexact); 128 = exact coefficients only (no fast attempt); the layout, cache
 // policy, priority and workgroup-order variants defined above.
 // A64: exactly 64 antennas and every in-item offset below 2^32 (the launcher checks), so no antenna is clamped.
-template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3, bool A64 = false>
+// Pow2: out_scale * 2^-14 is a power of two (requant_bits<true>: one exact FMA).
+template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3, bool A64 = false, bool Pow2 = false>
 __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -968,7 +969,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
   // packed bytes (16 VGPRs) stay live and the voltage registers of row i die after it.
   constexpr bool kTile = Full && !(Mode & (kSkipMfma | kSkipStore | kSkipLoad | kPolOrder));
   uint32_t pkall[2][NTS][4];
-  if constexpr (kTile) i8_contract_rows<Signed, NTS>(fr, d, colsum, s32, S8, lane, h, pkall);
+  if constexpr (kTile) i8_contract_rows<Signed, NTS, Pow2>(fr, d, colsum, s32, S8, lane, h, pkall);
   if constexpr ((Mode & kPrioStores) != 0) __builtin_amdgcn_s_setprio(3);
 
 #pragma unroll
@@ -1037,7 +1038,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
           if constexpr (kTile)
             pk[tau][i] = pkall[p][tau][i];
           else
-            pk[tau][i] = requant4<Signed>(acc[i][tau], colsum, 16 * tau + 4 * h, s32);
+            pk[tau][i] = requant4<Signed, Pow2>(acc[i][tau], colsum, 16 * tau + 4 * h, s32);
         }
         transpose_rows4(pk[tau]);
       }
@@ -1082,7 +1083,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
         // 4 M2 contiguous bytes: one 8- or 16-byte store per lane instead of 4 M2 byte stores
         uint32_t pk[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pk[i] = requant4<Signed>(acc[i][0], colsum, 4 * h, s32);
+        for (int i = 0; i < 4; ++i) pk[i] = requant4<Signed, Pow2>(acc[i][0], colsum, 4 * h, s32);
         if (h == 0) {
           const size_t orow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T) + 4 * tq;
           int8_t* o = reinterpret_cast<int8_t*>(P.y) + orow * M2;
@@ -1104,7 +1105,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(F
       for (int tau = 0; tau < NTS; ++tau) {
         if (!Full && tau >= nts) break;
         const int col0 = 16 * (tau0 + tau) + 4 * h;
-        const uint32_t packed = requant4<Signed>(acc[i][tau], colsum, 16 * tau + 4 * h, s32);
+        const uint32_t packed = requant4<Signed, Pow2>(acc[i][tau], colsum, 16 * tau + 4 * h, s32);
         if ((M2 & 3) == 0 && col0 + 4 <= M2) {
           *reinterpret_cast<uint32_t*>(o + col0) = packed;
         } else {
@@ -1135,12 +1136,16 @@ int launch_i8_item(FusedArgs P, hipStream_t st, size_t min_lds = 0) {
   BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many items");
   const char* ae = diag_env("BF_I8_A64");  // measurement: 0 forces the clamped per-lane addressing
   const bool a64 = P.A == 64 && 24ull * P.C * P.T * 4 + P.T * 4ull < (1ull << 32) && !(ae && ae[0] == '0');
-  if (a64)
-    hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ, true>),
-                       dim3(static_cast<unsigned>(n_items)), dim3(kThreads), lds, st, P);
+  const bool pow2 = scale_is_pow2(P.out_scale * 0x1p-14f);  // the requantisation's exact single FMA
+  const dim3 grid(static_cast<unsigned>(n_items)), block(kThreads);
+  if (a64 && pow2)
+    hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ, true, true>), grid, block, lds, st, P);
+  else if (a64)
+    hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ, true, false>), grid, block, lds, st, P);
+  else if (pow2)
+    hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ, false, true>), grid, block, lds, st, P);
   else
-    hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ, false>),
-                       dim3(static_cast<unsigned>(n_items)), dim3(kThreads), lds, st, P);
+    hipLaunchKernelGGL((beamform_fused_i8_item_kernel<Signed, NTS, Full, Mode, Occ, false, false>), grid, block, lds, st, P);
   BF_LAUNCHED("beamform_fused_i8_item_kernel");
 }
 

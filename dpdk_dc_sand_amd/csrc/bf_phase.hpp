@@ -118,6 +118,19 @@ __device__ __forceinline__ double steering_coeff_fast(float4 dv, double chc, dou
   return rot;
 }
 
+// Hardware phasor (measurement): the float64 rotation reduced to revolutions in float64 (u = rot / 2 pi - rint(.),
+// |u| <= 1/2), rounded once to float32, then v_sin_f32 / v_cos_f32 (which take revolutions).  The argument rounding
+// is <= 2^-26 rev (~2^-23.3 in the phasor); the instructions' own error is measured by
+// tools/probes/sincos_hw_probe.hip.
+__device__ __forceinline__ void steering_coeff_hw(float4 dv, double chc, double k, double dt, float* re, float* im) {
+  const double tau = fma(static_cast<double>(dv.y), dt, static_cast<double>(dv.x));
+  const double phi = fma(static_cast<double>(dv.w), dt, static_cast<double>(dv.z));
+  const double u = fma(tau * chc, k, phi) * 0.15915494309189535;  // 1 / (2 pi)
+  const float uf = static_cast<float>(u - rint(u));
+  *re = __builtin_amdgcn_cosf(uf);
+  *im = __builtin_amdgcn_sinf(uf);
+}
+
 // ---- Q14 phasors of the integer (int8-beam) path ----------------------------------------------------------------
 // Contract (oracle fused_beamform_int8): W = (rint(2^14 re), rint(2^14 im)) of the EXACT phasor (steering_coeff,
 // then the optional gain), ties to even.  q14_fast evaluates cos/sin of the reduced angle to ~1e-11 instead:

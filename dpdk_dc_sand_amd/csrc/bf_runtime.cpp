@@ -73,6 +73,26 @@ int cu_count() {
   return n;
 }
 
+AuxStream* aux_stream() {
+  static thread_local AuxStream per_device[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("aux stream: no current device");
+    return nullptr;
+  }
+  AuxStream& a = per_device[dev];
+  if (!a.stream) {
+    hipError_t e = hipStreamCreateWithFlags(&a.stream, hipStreamNonBlocking);
+    for (auto& ev : a.ev)
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      set_error("aux stream: %s", hipGetErrorString(e));
+      return nullptr;
+    }
+  }
+  return &a;
+}
+
 }  // namespace bf
 
 extern "C" {

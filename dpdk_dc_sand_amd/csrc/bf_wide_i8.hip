@@ -1044,6 +1044,11 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
   }
 }
 
+template <bool Signed, int Mode>
+int launch_w32t_contract(FusedArgs P, hipStream_t st);
+template <bool Signed, int Mode>
+int launch_w32_overlapped(FusedArgs P, int k, hipStream_t st);
+
 template <bool Signed, int Mode = 0>
 int launch_w32(FusedArgs P, hipStream_t st) {
   const size_t lds = w32_lds_bytes(P.A);
@@ -1072,8 +1077,32 @@ int launch_w32(FusedArgs P, hipStream_t st) {
       }
       return BF_OK;
     }
+    // measurement (BF_W32_OVERLAP = k chunks, diagnostic build): the generator's chunks on a second stream, each
+    // chunk's contraction on the caller's stream after its chunk of the table -- generator chunk i + 1 runs beside
+    // contraction chunk i (the contraction's chunk grid leaves CUs the generator's waves can use)
+    const char* ov = diag_env("BF_W32_OVERLAP");
+    const int nover = ov ? std::min(16, std::max(1, atoi(ov))) : 1;
+    if (nover > 1 && P.B == 1 && P.c_count == 0 && P.delay_channels == 1)
+      return launch_w32_overlapped<Signed, Mode>(P, nover, st);
     const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32, st);
     if (e != BF_OK) return e;
+    return launch_w32t_contract<Signed, Mode>(P, st);
+  }
+  if (P.gain)
+    hipLaunchKernelGGL((beamform_fused_i8_w32_kernel<Signed, Mode, true>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW8Threads), lds, st, P);
+  else
+    hipLaunchKernelGGL((beamform_fused_i8_w32_kernel<Signed, Mode, false>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW8Threads), lds, st, P);
+  BF_LAUNCHED("beamform_fused_i8_w32_kernel");
+}
+
+// The table-driven contraction of one launch (or channel chunk: P.c_count, pointers offset by the caller) whose
+// kLayoutW32 table is ready in P.table on `st`.
+template <bool Signed, int Mode>
+int launch_w32t_contract(FusedArgs P, hipStream_t st) {
+  const size_t lds = w32_lds_bytes(P.A);
+  {
     const int Cn = P.c_count ? P.c_count : P.C;
     const int npasses = ((((P.T >> 1) + 15) >> 4) + 3) >> 2;
     // config 4's shape walks 8 channels per workgroup (385.5 vs 389.4 us for 4, profiles/r3_ad*), the others 4
@@ -1101,13 +1130,42 @@ int launch_w32(FusedArgs P, hipStream_t st) {
       hipLaunchKernelGGL((beamform_fused_i8_w32t_kernel<Signed, Mode, false>), grid3, block, lds, st, P);
     BF_LAUNCHED("beamform_fused_i8_w32t_kernel");
   }
-  if (P.gain)
-    hipLaunchKernelGGL((beamform_fused_i8_w32_kernel<Signed, Mode, true>), dim3(static_cast<unsigned>(grid)),
-                       dim3(kW8Threads), lds, st, P);
-  else
-    hipLaunchKernelGGL((beamform_fused_i8_w32_kernel<Signed, Mode, false>), dim3(static_cast<unsigned>(grid)),
-                       dim3(kW8Threads), lds, st, P);
-  BF_LAUNCHED("beamform_fused_i8_w32_kernel");
+}
+
+// Generator and contraction overlapped over k channel chunks: fork the caller's stream to the aux stream, generate
+// every chunk's table there (event per chunk), and contract chunk i on the caller's stream once its table is done.
+// The aux stream waits for everything the caller queued before (a previous launch's contraction may still read
+// the workspace), and the caller's stream waits for every chunk, so the call stays stream-ordered for the caller.
+template <bool Signed, int Mode>
+int launch_w32_overlapped(FusedArgs P, int k, hipStream_t st) {
+  AuxStream* ax = aux_stream();
+  if (!ax) return BF_ERR_HIP;
+  const int per = (P.C + k - 1) / k;
+  BF_HIP(hipEventRecord(ax->ev[0], st));
+  BF_HIP(hipStreamWaitEvent(ax->stream, ax->ev[0], 0));
+  auto chunk = [&](int c0) {
+    FusedArgs Q = P;
+    Q.c_count = std::min(per, P.C - c0);
+    Q.raw = P.raw + static_cast<size_t>(c0) * P.T * 4;
+    Q.y = static_cast<int8_t*>(P.y) + static_cast<size_t>(c0) * P.T * 2 * P.M;
+    Q.table = P.table + static_cast<size_t>(c0) * ((P.M + 31) / 32) * 1024 * w32_table_steps(P.A);
+    Q.base_ch = P.base_ch + c0;
+    return Q;
+  };
+  int i = 0;
+  for (int c0 = 0; c0 < P.C; c0 += per, ++i) {
+    FusedArgs Q = chunk(c0);
+    const int e = launch_q14_table(Q, const_cast<uint32_t*>(Q.table), kLayoutW32, ax->stream);
+    if (e != BF_OK) return e;
+    BF_HIP(hipEventRecord(ax->ev[1 + i], ax->stream));
+  }
+  i = 0;
+  for (int c0 = 0; c0 < P.C; c0 += per, ++i) {
+    BF_HIP(hipStreamWaitEvent(st, ax->ev[1 + i], 0));
+    const int e = launch_w32t_contract<Signed, Mode>(chunk(c0), st);
+    if (e != BF_OK) return e;
+  }
+  return BF_OK;
 }
 
 }  // namespace

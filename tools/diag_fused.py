@@ -59,11 +59,22 @@ ROUNDS = int(_os.environ.get("DIAG_ROUNDS", "1"))
 if "wide" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_wide.argtypes = [I, I, V, V, V, I, I, I, I, I, I, D, V]
     wnames = {0: "full (fast coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 3: "no-coef,no-mfma",
-              5: "no-coef,no-store", 16: "nt stores", 32: "branchy phasor validity"}
+              5: "no-coef,no-store", 16: "nt stores", 32: "branchy phasor validity", 64: "hw sin/cos phasors",
+              1000: "buffer loads", 1001: "buffer loads, no-coef", 1004: "buffer loads, no-store",
+              1064: "buffer loads, hw sin/cos phasors"}
     if _os.environ.get("WIDE_MODES"):
         wnames = {int(m): wnames.get(int(m), str(m)) for m in _os.environ["WIDE_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
     for tw in [int(t) for t in _os.environ.get("WIDE_TW", "2,1").split(",")]:
+        ref = None
+        for mode in [m for m in wnames if m % 1000 in (0, 64)]:  # float beams of the full forms against mode 0
+            assert lib.bf_diag_wide(mode, tw, bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, B, C, T, A, M, Ctot, 1 / 1712e6,
+                                    q.handle) == 0
+            y = bufs[0][1].get(q).view(np.float32).astype(np.float64)
+            if ref is None:
+                ref = y
+            print(f"  wide tw={tw} mode {mode:4d} vs mode {min(wnames)}: max |dy| {np.abs(y - ref).max():.3e} "
+                  f"(max |y| {np.abs(ref).max():.3e})")
         res = {m: [] for m in wnames}
         for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
             for mode in wnames:
@@ -135,24 +146,34 @@ if "w32chunk" in _os.environ.get("DIAG_KERNELS", ""):  # generator + contraction
     lib.bf_diag_w32_launch.argtypes = [V, V, V, V, I, I, I, I, I, I, D, V]
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
     tb2 = accel.DeviceArray(ctx, (B * C * ((M + 31) // 32) * 1024 * 8 + 4096,), np.uint32)
-    chunks = [int(v) for v in _os.environ.get("W32_CHUNKS", "1,2,4,8").split(",")]
+    # "n": generator + contraction alternated over n channel chunks on one stream; "oN": the generator's N chunks on
+    # a second stream beside the contraction chunks (BF_W32_OVERLAP)
+    chunks = _os.environ.get("W32_CHUNKS", "1,2,4,8").split(",")
+
+    def set_chunks(n):
+        _os.environ["BF_W32_CHUNKS"] = "1" if n.startswith("o") else n
+        _os.environ["BF_W32_OVERLAP"] = n[1:] if n.startswith("o") else "1"
     outs, res = {}, {n: [] for n in chunks}
     for n in chunks:
-        _os.environ["BF_W32_CHUNKS"] = str(n)
+        set_chunks(n)
         _lib.call("bf_memset", bufs[0][1].ptr, 0, nout // 4, q.handle)
         assert lib.bf_diag_w32_launch(bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, tb2.ptr, B, C, T, A, M, Ctot,
                                       1 / 1712e6, q.handle) == 0
+        q.finish()
         outs[n] = bufs[0][1].get(q)[: nout // 4].copy()
-    print("  chunked == whole launch (int8 beams):", all(np.array_equal(outs[chunks[0]], o) for o in outs.values()))
+    print("  chunked / overlapped == whole launch (int8 beams):",
+          all(np.array_equal(outs[chunks[0]], o) for o in outs.values()))
     for r in range(ROUNDS):
         for n in chunks:
-            _os.environ["BF_W32_CHUNKS"] = str(n)
+            set_chunks(n)
             res[n].append(timeit(lambda i: lib.bf_diag_w32_launch(bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
                                                                   tb2.ptr, B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
     for n in chunks:
         ts = sorted(res[n])
-        print(f"  generator + contraction, {n} channel chunk(s): median {ts[len(ts) // 2] * 1e6:8.1f} us")
+        kind = f"{n[1:]} chunk(s) overlapped on two streams" if n.startswith("o") else f"{n} channel chunk(s)"
+        print(f"  generator + contraction, {kind}: median {ts[len(ts) // 2] * 1e6:8.1f} us")
     _os.environ.pop("BF_W32_CHUNKS")
+    _os.environ.pop("BF_W32_OVERLAP")
 if "w8" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_w8.argtypes = [I, V, V, V, I, I, I, I, I, I, D, V]
     w8names = {0: "full (fast+fixup)", 128: "exact-only coef", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load",
