@@ -651,19 +651,19 @@ __global__ __launch_bounds__(NW * 64, Occ) void beamform_table_os_kernel(const u
   __syncthreads();
   // chunk pairs: kc in LDS buffer 0, kc + 1 in buffer 1; each chunk's successor table is requested before the chunk
   // is contracted (its voltages right after the re-deal: vmcnt is in order, so the table conversion waits for the
-  // table only).  The last pair requests nothing past the item (peeled, no clamped re-read).
-  auto pair = [&](int kc, auto more) __attribute__((always_inline)) {
-    tload(kc + 1);
+  // table only).  The last pair requests nothing past the item: a uniform branch in the one loop -- peeled, the last
+  // pair kept its own copies of the loop's thread-index offsets live across the loop (spills).
+  for (int kc = 0; kc < nk; kc += 2) {  // one loop, the last pair's successor requests skipped by a uniform branch
+    tload(min(kc + 1, nk - 1));
     contract(0, xr, kc + 1);
     tstore(1);
     __syncthreads();
-    if constexpr (decltype(more)::value) tload(kc + 2);
-    contract(1, xr, decltype(more)::value ? kc + 2 : -1);
-    if constexpr (decltype(more)::value) tstore(0);
+    const bool more = kc + 2 < nk;
+    if (more) tload(kc + 2);
+    contract(1, xr, more ? kc + 2 : -1);
+    if (more) tstore(0);
     __syncthreads();
-  };
-  for (int kc = 0; kc + 2 < nk; kc += 2) pair(kc, std::true_type{});
-  pair(nk - 2, std::false_type{});
+  }
 
 #pragma unroll
   for (int rg = 0; rg < RG; ++rg) {
@@ -779,7 +779,10 @@ template <bool Signed>
 int dispatch_table(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                    hipStream_t st) {
   const char* os = diag_env("BF_TABLE_OS");  // measurement: 0 keeps the slab kernels
-  if (table_os_fits(NB, A, M, x, w) && !(os && os[0] == '0')) return launch_table_os<Signed>(x, w, y, bpc, A, st);
+  // 4 waves per item (256 VGPRs, two workgroups per CU), spill-free in the one-loop form.  The 8-wave form (128
+  // VGPRs) ran 2 % faster in its peeled form (801 vs 819 us at config 4, profiles/r4_c_table_os_ab.txt) but spills
+  // 24-40 B/lane in either form; bounded to 3 waves per SIMD it fits, but one workgroup per CU runs 903 us
+  if (table_os_fits(NB, A, M, x, w) && !(os && os[0] == '0')) return launch_table_os<Signed, 0, 4>(x, w, y, bpc, A, st);
   // Long rows (>= 16 k-steps: 256+ antennas): the widest slab whose staged fragments leave room for a second
   // workgroup per CU, so one workgroup's table staging overlaps the other's contraction (cfg4: a 128 KiB slab held
   // one workgroup per CU and ran 3.1 ms); the slabs' re-reads of x hit L2 (XCD-grouped slabs).

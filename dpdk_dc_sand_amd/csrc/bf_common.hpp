@@ -87,6 +87,7 @@ inline bool q14_sum_bound_ok(int A, bool sample_signed, double max_gain) {
 // Compute units of the current device (cached per device index; sizes persistent grids only).
 int cu_count();
 
+#ifdef BF_DIAG
 // A second stream on the current device for work a call forks off its caller's stream and joins back (the int8
 // wide path's coefficient generator running beside the contraction), and a pool of events for the hand-offs.
 // Thread-local per device: concurrent callers on other host threads never serialise on one another's helper.
@@ -96,5 +97,6 @@ struct AuxStream {
   hipEvent_t ev[17] = {};  // [0] fork, [1 + k] chunk k done
 };
 AuxStream* aux_stream();
+#endif
 
 }  // namespace bf

@@ -73,6 +73,7 @@ int cu_count() {
   return n;
 }
 
+#ifdef BF_DIAG  // the generator/contraction overlap measurement (bf_wide_i8.hip)
 AuxStream* aux_stream() {
   static thread_local AuxStream per_device[64];
   int dev = 0;
@@ -92,6 +93,7 @@ AuxStream* aux_stream() {
   }
   return &a;
 }
+#endif
 
 }  // namespace bf
 

@@ -1046,8 +1046,10 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
 
 template <bool Signed, int Mode>
 int launch_w32t_contract(FusedArgs P, hipStream_t st);
+#ifdef BF_DIAG
 template <bool Signed, int Mode>
 int launch_w32_overlapped(FusedArgs P, int k, hipStream_t st);
+#endif
 
 template <bool Signed, int Mode = 0>
 int launch_w32(FusedArgs P, hipStream_t st) {
@@ -1077,13 +1079,15 @@ int launch_w32(FusedArgs P, hipStream_t st) {
       }
       return BF_OK;
     }
-    // measurement (BF_W32_OVERLAP = k chunks, diagnostic build): the generator's chunks on a second stream, each
-    // chunk's contraction on the caller's stream after its chunk of the table -- generator chunk i + 1 runs beside
-    // contraction chunk i (the contraction's chunk grid leaves CUs the generator's waves can use)
+#ifdef BF_DIAG
+    // measurement (BF_W32_OVERLAP = k chunks): the generator's chunks on a second stream, each chunk's contraction
+    // on the caller's stream after its chunk of the table.  Measured slower than the serial pair (round 4,
+    // profiles/r4_c_w32_overlap_ab.txt: 2 / 4 / 8 chunks 493 / 518 / 852 vs 466 us), so diagnostic only.
     const char* ov = diag_env("BF_W32_OVERLAP");
     const int nover = ov ? std::min(16, std::max(1, atoi(ov))) : 1;
     if (nover > 1 && P.B == 1 && P.c_count == 0 && P.delay_channels == 1)
       return launch_w32_overlapped<Signed, Mode>(P, nover, st);
+#endif
     const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32, st);
     if (e != BF_OK) return e;
     return launch_w32t_contract<Signed, Mode>(P, st);
@@ -1132,6 +1136,7 @@ int launch_w32t_contract(FusedArgs P, hipStream_t st) {
   }
 }
 
+#ifdef BF_DIAG
 // Generator and contraction overlapped over k channel chunks: fork the caller's stream to the aux stream, generate
 // every chunk's table there (event per chunk), and contract chunk i on the caller's stream once its table is done.
 // The aux stream waits for everything the caller queued before (a previous launch's contraction may still read
@@ -1167,6 +1172,7 @@ int launch_w32_overlapped(FusedArgs P, int k, hipStream_t st) {
   }
   return BF_OK;
 }
+#endif  // BF_DIAG
 
 }  // namespace
 

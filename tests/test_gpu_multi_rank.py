@@ -136,6 +136,7 @@ def test_bench_rccl_scatter_path_one_rank(tmp_path):
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
     sc = line["scatter"]
+    assert "error" not in sc, sc
     assert sc["backend"] == "rccl" and sc["ranks"] == 1 and "RCCL" in sc["collective"], sc
     assert line["scatter_ok"] is True and sc["verified"] is True, sc
     # three timed scatters + nothing else, all through ncclRecv (the self send/recv at one rank)

@@ -117,12 +117,14 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
     lib.bf_diag_i8_os.argtypes = [I, V, V, V, I, I, I, I, I, V]
 
     def w32t_call(mode, i):
-        if mode >= 700:
+        if 700 <= mode < 900:
             return lib.bf_diag_i8_os(mode - 700, bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, tb.ptr, B, C, T, A, M, q.handle)
         return lib.bf_diag_w32_table(mode, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr, tb.ptr, B, C, T, A, M, Ctot,
                                      1 / 1712e6, q.handle)
-    for mode in tnames:
-        assert mode < 0 or w32t_call(mode, 0) == 0, mode
+    for mode in list(tnames):
+        if mode >= 0 and w32t_call(mode, 0) != 0:
+            print(f"  w32t mode {mode}: launch failed: {lib.bf_last_error().decode(errors='replace')}")
+            tnames.pop(mode)
     for alt in (220, 240, 260, 280, 700, 900, 920, 940):  # another form's int8 beams, same input and table: bitwise equal
         if alt not in tnames:
             continue
