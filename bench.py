@@ -179,12 +179,12 @@ def scatter_inputs(args, dist, shape):
             times.append(time.perf_counter() - t0)
         t = dist.max(min(times))
         # what arrived is what the root sent: per-rank slice checksums against the root's band (on the devices)
-        ok, per_rank = dist.comm.verify(band, out, B, A, C, T, args.queue)
+        ok, sums = dist.comm.verify(band, out, B, A, C, T, args.queue)
         sent, received = dist.comm.stats()
         del band
         report["verified"] = ok
-        if per_rank is not None:
-            report["checksums"] = per_rank
+        if sums is not None:
+            report["checksums"] = sums
         report["rccl_bytes_received_this_rank"] = received
         report["rccl_bytes_sent_root"] = sent if rank == 0 else None
         report["collective"] = ("RCCL grouped ncclSend/ncclRecv over xGMI via libbf bf_channel_scatter, device to "
@@ -411,6 +411,8 @@ def cpu_baseline(wl, out_int8, seconds=10.0):
     rate = A * 2 * c * T * B / dt / 1e9
     return {"value": round(rate, 4), "unit": "Gsamples/s", "cores": int(threads), "blas_threads": int(threads),
             "host_cpus_in_affinity": affinity, "cgroup_cpu_quota_cores": quota, "kind": "port",
+            "threads_note": "BLAS threads = the affinity mask's CPUs, capped by the BLAS library's own thread maximum; "
+                            "the cgroup quota bounds the CPU time those threads get",
             "sample": f"{c} of {wl['C']} channels x B={B} x T={T} x A={A} x 2 pols ({dt:.1f} s), extrapolated "
                       f"linearly in channels: oracle.fused_beamform (NumPy reorder + float64-phase coefficients "
                       f"with delay/phase rates + float32 matmul{' + requantise' if out_int8 else ''}, "

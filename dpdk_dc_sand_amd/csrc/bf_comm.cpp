@@ -20,6 +20,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 
@@ -92,6 +93,8 @@ int rccl_fail(ncclResult_t e, const char* what) {
   } while (0)
 
 }  // namespace
+
+constexpr size_t kScatterChunk = size_t(256) << 20;  // bytes per RCCL group of a scatter (whole rows)
 
 struct bf_comm {
   ncclComm_t comm = nullptr;
@@ -214,6 +217,10 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
   const size_t pitch = run * static_cast<size_t>(c->nranks);    // the band's (b, a) row
   const size_t rows = static_cast<size_t>(B) * A;
   const size_t slice_bytes = run * rows;
+  // The slice moves in blocks of whole (b, a) rows of at most kScatterChunk bytes, one RCCL group per block: on the
+  // one-GPU box a single 2 GiB self send/recv (or its 2-D pack) left the second GiB of the slice unwritten
+  // (tools/diag_scatter.py: every slice up to 1 GiB arrived intact, 2047 and 2048 MiB did not).
+  const size_t rows_per = std::max<size_t>(1, kScatterChunk / run);
   if (c->rank == root) {
     const size_t need = slice_bytes * static_cast<size_t>(c->nranks);
     if (need > c->staging_bytes) {
@@ -229,23 +236,30 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
     // the previous scatter's sends may still read the staging buffer on another stream
     BF_HIP(hipStreamWaitEvent(st, c->sent, 0));
     uint8_t* stg = static_cast<uint8_t*>(c->staging);
-    for (int r = 0; r < c->nranks; ++r)
-      BF_HIP(hipMemcpy2DAsync(stg + slice_bytes * static_cast<size_t>(r), run, band + run * static_cast<size_t>(r),
-                              pitch, run, rows, hipMemcpyDeviceToDevice, st));
-    BF_RCCL(rccl().group_start());
-    for (int r = 0; r < c->nranks; ++r) {
-      ncclResult_t e = rccl().send(stg + slice_bytes * static_cast<size_t>(r), slice_bytes, ncclUint8, r, c->comm, st);
-      if (e == ncclSuccess && r == root) e = rccl().recv(slice, slice_bytes, ncclUint8, root, c->comm, st);
-      if (e != ncclSuccess) {
-        (void)rccl().group_end();
-        return rccl_fail(e, r == root ? "ncclSend/ncclRecv (self)" : "ncclSend");
+    for (size_t r0 = 0; r0 < rows; r0 += rows_per) {
+      const size_t nr = std::min(rows_per, rows - r0), off = r0 * run, bytes = nr * run;
+      for (int r = 0; r < c->nranks; ++r)
+        BF_HIP(hipMemcpy2DAsync(stg + slice_bytes * static_cast<size_t>(r) + off, run,
+                                band + r0 * pitch + run * static_cast<size_t>(r), pitch, run, nr,
+                                hipMemcpyDeviceToDevice, st));
+      BF_RCCL(rccl().group_start());
+      for (int r = 0; r < c->nranks; ++r) {
+        ncclResult_t e = rccl().send(stg + slice_bytes * static_cast<size_t>(r) + off, bytes, ncclUint8, r, c->comm, st);
+        if (e == ncclSuccess && r == root) e = rccl().recv(slice + off, bytes, ncclUint8, root, c->comm, st);
+        if (e != ncclSuccess) {
+          (void)rccl().group_end();
+          return rccl_fail(e, r == root ? "ncclSend/ncclRecv (self)" : "ncclSend");
+        }
       }
+      BF_RCCL(rccl().group_end());
     }
-    BF_RCCL(rccl().group_end());
     BF_HIP(hipEventRecord(c->sent, st));
     c->p2p_sent += slice_bytes * static_cast<unsigned long long>(c->nranks);
   } else {
-    BF_RCCL(rccl().recv(slice, slice_bytes, ncclUint8, root, c->comm, st));
+    for (size_t r0 = 0; r0 < rows; r0 += rows_per) {
+      const size_t nr = std::min(rows_per, rows - r0);
+      BF_RCCL(rccl().recv(slice + r0 * run, nr * run, ncclUint8, root, c->comm, st));
+    }
   }
   c->p2p_received += slice_bytes;
   BF_HIP(hipEventRecord(c->done, st));
