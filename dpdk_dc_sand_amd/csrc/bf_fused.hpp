@@ -111,15 +111,21 @@ __device__ __forceinline__ void lds_barrier() {
 // Kernel-path override of a launch (flags & BF_FUSED_PATH_MASK): 0 automatic, else one of the BF_FUSED_PATH_* values.
 inline int fused_kernel_choice(const FusedArgs& P) { return P.path; }
 
-// Q14 coefficient tables (bf_q14table.hip): (B, C, M, A) words, or the 32-beam int8 kernel's item layout.
-constexpr int kLayoutNatural = 0, kLayoutW32 = 1;
+// Q14 coefficient tables (bf_q14table.hip): (B, C, M, A) words, the 32-beam int8 kernel's item layout, or the
+// halved limb image of the config-4 int8 kernel (kLayoutW32H: per (b, c, 32-beam slab) the LDS image the contraction
+// copies verbatim -- [step][tile][limb][lane] x 16 bytes of (Wc, -Ws) limb pairs, 1024 words per k-step -- then a
+// 256-word block whose first 64 words are the slab's per-beam column sums (sum_a Wc, sum_a Ws)).
+constexpr int kLayoutNatural = 0, kLayoutW32 = 1, kLayoutW32H = 2;
+constexpr int kW32HSumWords = 256;  // the column-sum block of a kLayoutW32H item (64 words used)
+__host__ __device__ inline int w32h_item_words(int Sp) { return 1024 * Sp + kW32HSumWords; }
 // k-steps of 32 antennas of the 32-beam int8 kernel, padded to a multiple of 4 (its four-buffer rotation)
 __host__ __device__ inline int w32_table_steps(int A) { return 4 * ((((A + 31) >> 5) + 3) / 4); }
 // The table-driven 32-beam kernel stages at most 4 units of 8 words per thread: Sp <= 8 (A <= 256).
 __host__ __device__ inline bool w32_table_fits(int A) { return w32_table_steps(A) <= 8; }
-// Bytes of the kLayoutW32 table of one launch: 1024 Sp words per (b, c, 32-beam slab).
+// Bytes of the int8 wide path's coefficient table of one launch: w32h_item_words(Sp) words per (b, c, 32-beam slab)
+// (kLayoutW32 uses the first 1024 Sp of them).
 inline size_t w32_table_bytes(int B, int C, int A, int M) {
-  return static_cast<size_t>(B) * C * ((M + 31) / 32) * 1024 * w32_table_steps(A) * 4;
+  return static_cast<size_t>(B) * C * ((M + 31) / 32) * w32h_item_words(w32_table_steps(A)) * 4;
 }
 int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t st);
 

@@ -455,12 +455,39 @@ __device__ __forceinline__ void w32_frags(const u32x2_t (&d)[8], i32x4_t (&f)[2]
     }
 }
 
+// The step's second B fragments [x_im, ~x_re] per pol and sample: the halved limb image's y_im operand (~x = -x - 1
+// stays in int8 where -x overflows at -128; the bias is sum_a Ws per beam, removed at requantisation).  Per raw dword
+// one xor (the re bytes of both pols; unsigned samples: x - 128 in the im bytes, ~(x - 128) in the re bytes) and per
+// fragment dword one v_perm.
+template <bool Signed = true>
+__device__ __forceinline__ void w32_frags_im(const u32x2_t (&d)[8], i32x4_t (&f)[2][2]) {
+  constexpr uint32_t kFlip = Signed ? 0x00ff00ffu : 0x807f807fu;
+  uint32_t nd[8][2];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    nd[q][0] = d[q].x ^ kFlip;
+    nd[q][1] = d[q].y ^ kFlip;
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint32_t w[4];
+#pragma unroll
+      for (int m2 = 0; m2 < 4; ++m2)
+        w[m2] = __builtin_amdgcn_perm(nd[2 * m2 + 1][i], nd[2 * m2][i], p ? 0x06070203u : 0x04050001u);
+      f[p][i] = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]), static_cast<int>(w[3])};
+    }
+}
+
 // 32 MFMAs of one step: per tile t (16 real columns) the two limbs' A fragments from LDS, 2 pols x 2 samples.
 template <int Mode>
-__device__ __forceinline__ void w32_mfma(const int4* __restrict__ fr, int s, int lane, const i32x4_t (&f)[2][2],
-                                         i32x4_t (&hi)[2][2][4], i32x4_t (&lo)[2][2][4]) {
+__device__ __forceinline__ void w32_mfma(const int4* __restrict__ fr, int s, int lane, const i32x4_t (&f0)[2][2],
+                                         i32x4_t (&hi)[2][2][4], i32x4_t (&lo)[2][2][4],
+                                         const i32x4_t (&f1)[2][2] = {}) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
+    const i32x4_t (&f)[2][2] = (Mode & 16) && t >= 2 ? f1 : f0;  // measurement: tiles 2, 3 on the second fragments
     const int4 x0 = fr[(((s * 4 + t) * 2 + 0) * 64) + lane];
     const int4 x1 = fr[(((s * 4 + t) * 2 + 1) * 64) + lane];
     const i32x4_t chi = i32x4_t{x0.x, x0.y, x0.z, x0.w}, clo = i32x4_t{x1.x, x1.y, x1.z, x1.w};
@@ -922,12 +949,13 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
         for (int s = 0; s < kSp; ++s) {
           constexpr int dummy = 0;
           (void)dummy;
-          i32x4_t f[2][2];
+          i32x4_t f[2][2], fi[2][2];
           const int j = (pass * kSp + s) % NB;
           w32_frags<Signed>(db[j], f);
+          if constexpr ((Mode & 16) != 0) w32_frags_im(db[j], fi);
           __builtin_amdgcn_sched_barrier(0);
           issue(db[j]);
-          w32_mfma<0>(lds4, s, lane, f, hi, lo);
+          w32_mfma<Mode & 16>(lds4, s, lane, f, hi, lo, fi);
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
@@ -1044,12 +1072,521 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
   }
 }
 
+// ---- the halved-image contraction at config 4's shape (the default with a workspace there) ----------------------
+// The table (q14_image_kernel, kLayoutW32H) is the LDS image itself: per (b, c, slab) the (Wc, -Ws) limb fragments of
+// 32 beams x 8 k-steps (32 KiB, half the w32t kernel's image) and the slab's column sums.  A workgroup copies the
+// next channel's image into the other of two LDS buffers by LDS-DMA (global_load_lds_dwordx4, 33 x 1 KiB) as the
+// current channel starts -- no table registers, no expansion, no table latency at the channel barrier -- and every
+// k-step builds two B fragments per pol and sample, [x_re, x_im] for y_re and [x_im, ~x_re] for y_im
+// (w32_frags_im), against the same A fragments: 32 MFMAs per step as before, half the LDS fragment reads.
+//   y_re = sum x_re Wc + x_im (-Ws)                            (+ 128 sum (Wc - Ws) for unsigned samples)
+//   y_im = sum x_im Wc + ~x_re (-Ws) - sum Ws                  (+ 128 sum (Wc + Ws) for unsigned samples)
+// Shape: 8 k-steps (224 < A <= 256), T = 256 (2 passes of 8 straight-line steps per wave, 2-buffer voltage ring),
+// M % 32 == 0, voltage offsets within a workgroup and the beams below 2^31 bytes; 8 channels per workgroup.  The DMA's completion is never waited for explicitly: it is issued before
+// the channel's first refill of the voltage ring, and vmcnt retires in order, so the compiler's own wait for any later
+// voltage load (long before the channel ends) covers it; the LDS reads of the other buffer need no wait at all (the
+// compiler does not see the DMA, so it inserts none).
+constexpr int kW32HChannels = 8;
+constexpr int kW32HItemWords = 8 * 1024 + kW32HSumWords;  // w32h_item_words(8)
+
+// y_im's B fragment from y_re's: [x_re, x_im, ...] -> [x_im, ~x_re, ...] per antenna (one xor + one v_perm per
+// dword; the same for unsigned samples, whose fragments already hold x - 128).
+__device__ __forceinline__ i32x4_t frag_im(const i32x4_t& f) {
+  i32x4_t r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t n = static_cast<uint32_t>(f[q]) ^ 0x00ff00ffu;
+    r[q] = static_cast<int>(__builtin_amdgcn_perm(n, n, 0x02030001u));
+  }
+  return r;
+}
+
+// The two LDS image buffers as distinct objects: the compiler's alias analysis then knows that an LDS-DMA into one
+// and the ds_reads of the other never overlap, and its own s_waitcnt bookkeeping covers the DMA (it counts it in
+// vmcnt and waits for it only before reading the buffer it writes).  With one array indexed by the channel parity it
+// waited vmcnt(0) before every fragment read; with the DMA hidden in inline asm it over-waited on the voltage ring.
+__shared__ __attribute__((aligned(16))) int4 w32h_img0[kW32HItemWords / 4];
+__shared__ __attribute__((aligned(16))) int4 w32h_img1[kW32HItemWords / 4];
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// Mode (diagnostics only): 16 the y_im MFMAs on y_re's fragment xor a constant (half the frag_im VALU; wrong beams),
+// 128 per-wave s_memtime phase cycles -> P.gain as uint64 [block][wave][4]: waiting for the step's voltages (to the
+// first fragment), the rest of the steps, requantise + stores, the channel barrier.
+template <bool Signed, bool Pow2, int Mode = 0>
+__global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32h_kernel(FusedArgs P) {
+  constexpr int Sp = 8, NP = 2, NB = 2, kCh = kW32HChannels;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const int C = P.C;
+  const int gpb = (C + kCh - 1) / kCh;  // channel groups per batch
+  int slab, grp;
+  if (P.xcd_order) {  // the slabs of one channel group back to back on one XCD: the second re-reads from L2
+    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
+    slab = local % P.nslabs;
+    grp = (local / P.nslabs) * 8 + x;
+    if (grp >= P.B * gpb) return;
+  } else {
+    slab = blockIdx.x % P.nslabs;
+    grp = blockIdx.x / P.nslabs;
+  }
+  const int b = grp / gpb, c0 = (grp - b * gpb) * kCh;
+  const int nk = min(kCh, C - c0);
+  const int m0 = slab * kW32Beams;
+  const size_t ant_stride = static_cast<size_t>(C) * P.T * 4;
+  const uint32_t hoff = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride);
+  const uint32_t ch_bytes = static_cast<uint32_t>(P.T) * 4;
+  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * C + c0) * static_cast<size_t>(P.T) * 4;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);  // (tid >> 6 is not provably uniform)
+  // the table as a buffer resource (the host checks its size < 2^31)
+  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(P.table), 0, 0x7fffffff,
+                                                                        0x00020000);
+  const uint32_t titem = static_cast<uint32_t>(((b * C + c0) * P.nslabs + slab) * kW32HItemWords * 4);
+  const uint32_t tch = static_cast<uint32_t>(P.nslabs * kW32HItemWords * 4);  // bytes per channel
+  const uint32_t lvoff = 16u * static_cast<uint32_t>(lane);
+  // half hf of this wave's part of channel kc's item -> image buffer img: 4 of the 32 one-KiB image pieces, and the
+  // wave's quarter of the 1 KiB column-sum block (both halves copy it: the same bytes twice, so they are alike)
+  auto dma_half = [&](int kc, int4* img, int hf) {
+    const uint32_t src = titem + static_cast<uint32_t>(kc) * tch;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pc = wave_u + 4 * (k + 4 * hf);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void_ptr)(img + 64 * pc), 16, lvoff,
+                                               src + 1024u * static_cast<uint32_t>(pc), 0, 0);
+    }
+    const int cs = 8192 + 64 * wave_u;  // words
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void_ptr)(reinterpret_cast<int*>(img) + cs), 4,
+                                             lvoff >> 2, src + 4u * static_cast<uint32_t>(cs), 0, 0);
+  };
+
+  // the voltage prefetch: step ls of pass lp of channel lk next, across the workgroup's channels
+  const int total = nk * NP * Sp;
+  int issued = 0, ls = 0, lp = 0, lk = 0;
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7fffffff,
+                                                                        0x00020000);
+  // T = 256: a wave's sample pairs (wave + 4 pass) * 16 + tl never need the clamp; the lane's part of the offset is
+  // one constant VGPR, the rest (step, pass, channel) goes to the SGPR offset
+  const uint32_t lvo = hoff + 8u * static_cast<uint32_t>(tl);
+  auto issue = [&](u32x2_t (&d)[8]) {
+    const uint32_t sbase = static_cast<uint32_t>(w8_step_base(ls, P.A)) * static_cast<uint32_t>(ant_stride) +
+                           static_cast<uint32_t>(lk) * ch_bytes + static_cast<uint32_t>(wave_u + 4 * lp) * 128u;
+    w32_load_buf<0>(vrs, lvo, sbase, static_cast<uint32_t>(ant_stride), d);
+    ++issued;  // selects, not branches; past the last step it repeats that step
+    const bool adv = issued < total;
+    const bool wrap = ls + 1 == Sp, pwrap = lp + 1 == NP;
+    ls = adv ? (wrap ? 0 : ls + 1) : ls;
+    lp = (adv && wrap) ? (pwrap ? 0 : lp + 1) : lp;
+    lk = (adv && wrap && pwrap) ? lk + 1 : lk;
+  };
+  u32x2_t db[NB][8];
+  dma_half(0, w32h_img0, 0);
+  dma_half(0, w32h_img0, 1);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) issue(db[j]);
+  // every wave's part of channel 0's image landed (all but the 16 voltage loads issued after it) before the barrier
+  __builtin_amdgcn_s_waitcnt(0x4f70);  // vmcnt(16): vmcnt[3:0] = 0, [15:14] = 1
+  lds_barrier();
+
+  const float s32 = P.out_scale * 0x1p-14f;
+  const int M2 = 2 * P.M;
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(P.y, 0, 0x7fffffff, 0x00020000);
+  // the lane's part of a beam-row store offset (sample 2 tl + i of the wave's 32, row piece of lane group h)
+  const uint32_t so_lane = static_cast<uint32_t>(2 * tl * M2 + 16 * (h >> 1) + 32 * (h & 1));
+  unsigned long long st_w = 0, st_m = 0, st_s = 0, st_b = 0, st_t = 0;
+  auto stamp = [&]() -> unsigned long long {
+    if constexpr ((Mode & 128) != 0) return __builtin_amdgcn_s_memtime();
+    return 0ull;
+  };
+  // one channel on image buffer `img` (the next channel's image DMA'd into `nxt`, half in each pass after step 1's
+  // refill; the last channel re-copies itself there, unread)
+  auto channel = [&](int kc, int4* img, int4* nxt) {
+    const int c = c0 + kc;
+    const int knext = min(kc + 1, nk - 1);
+    const int* csums = reinterpret_cast<const int*>(img) + 8192;  // [beam][sum Wc, sum Ws] of the slab
+#pragma unroll 1
+    for (int pass = 0; pass < NP; ++pass) {
+      i32x4_t rh[2][2][2], rl[2][2][2], ih[2][2][2], il[2][2][2];  // [pol][sample i][tile]
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) rh[p][i][t] = rl[p][i][t] = ih[p][i][t] = il[p][i][t] = i32x4_t{0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < Sp; ++s) {
+        const int j = s % NB;  // (Sp * pass is even)
+        i32x4_t f[2][2];
+        const unsigned long long t0 = stamp();
+        w32_frags<Signed>(db[j], f);
+        if constexpr ((Mode & 128) != 0) {  // the fragments exist: the voltage wait is over
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("" ::"v"(f[0][0][0]), "v"(f[1][1][3]));
+          const unsigned long long t1 = stamp();
+          st_w += t1 - t0;
+          st_t = t1;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        issue(db[j]);
+        if (s == 1) dma_half(knext, nxt, pass);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int4 x0 = img[((s * 2 + t) * 2 + 0) * 64 + lane];
+          const int4 x1 = img[((s * 2 + t) * 2 + 1) * 64 + lane];
+          const i32x4_t ahi = i32x4_t{x0.x, x0.y, x0.z, x0.w}, alo = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              // y_im's fragment rebuilt per tile (2 VALU per dword): fewer live registers than keeping all four
+              const i32x4_t fi = (Mode & 16) ? (f[p][i] ^ 0x00ff00ff) : frag_im(f[p][i]);
+              rh[p][i][t] = mfma_i8(ahi, f[p][i], rh[p][i][t]);
+              rl[p][i][t] = mfma_i8(alo, f[p][i], rl[p][i][t]);
+              ih[p][i][t] = mfma_i8(ahi, fi, ih[p][i][t]);
+              il[p][i][t] = mfma_i8(alo, fi, il[p][i][t]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr ((Mode & 128) != 0) st_m += stamp() - st_t;
+      }
+      const unsigned long long ts0 = stamp();
+      // requantise + store: lane (tl, h) holds beams 16 t + 4 h + r (re and im) of samples 2 tq2 + i; per tile two
+      // dwords [re, im, re, im] (beams 4h, 4h+1 | 4h+2, 4h+3) = bytes [32 t + 8 h, + 8) of the slab's 64-byte row.
+      // One permlane16_swap per dword pair gives lane group h the 16 bytes at 16 (h >> 1) + 32 (h & 1).
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const size_t prow = ((static_cast<size_t>(b) * 2 + p) * C + c) * static_cast<size_t>(P.T);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          uint32_t pk[2][2];  // [tile][dword]
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            // the bias corrections of beams 16 t + 4 h + r from the column sums (sum Wc, sum Ws)
+            const int4 q0 = *reinterpret_cast<const int4*>(csums + 2 * (16 * t + 4 * h));
+            const int4 q1 = *reinterpret_cast<const int4*>(csums + 2 * (16 * t + 4 * h) + 4);
+            const int wc[4] = {q0.x, q0.z, q1.x, q1.z}, ws[4] = {q0.y, q0.w, q1.y, q1.w};
+            uint32_t qr[4], qi[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int cre = Signed ? 0 : 128 * (wc[r] - ws[r]);
+              const int cim = Signed ? -ws[r] : 128 * (wc[r] + ws[r]) - ws[r];
+              qr[r] = requant_bits<Pow2>((rh[p][i][t][r] << 8) + rl[p][i][t][r] + cre, s32);
+              qi[r] = requant_bits<Pow2>((ih[p][i][t][r] << 8) + il[p][i][t][r] + cim, s32);
+            }
+            pk[t][0] = pack_low_bytes(qr[0], qi[0], qr[1], qi[1]);
+            pk[t][1] = pack_low_bytes(qr[2], qi[2], qr[3], qi[3]);
+          }
+          const auto sw0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+          const auto sw1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+          // through a buffer resource on the beams (32-bit offsets; the host checks the size): the row's base is
+          // wave-uniform (an SGPR soffset), the lane's part one VGPR -- no 64-bit address arithmetic per store
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4_t, u32x4_t{sw0[0], sw1[0], sw0[1], sw1[1]}), yrs, so_lane,
+              static_cast<uint32_t>((prow + 2 * (wave_u + 4 * pass) * 16 + i) * M2 + 2 * m0), 0);
+        }
+      }
+      if constexpr ((Mode & 128) != 0) st_s += stamp() - ts0;
+    }
+    const unsigned long long tb0 = stamp();
+    // this wave's DMA into `nxt` has landed (the compiler waits for it only before reading `nxt` itself, after the
+    // barrier -- too late for the other waves): everything but the 6 x 8 refills and 4 stores issued after it
+    asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
+    lds_barrier();  // every wave is done with `img`; `nxt` is complete
+    if constexpr ((Mode & 128) != 0) st_b += stamp() - tb0;
+  };
+  for (int kc = 0; kc < nk; kc += 2) {  // (two copies of the body: each reads one buffer, DMAs into the other)
+    channel(kc, w32h_img0, w32h_img1);
+    if (kc + 1 < nk) channel(kc + 1, w32h_img1, w32h_img0);
+  }
+  if constexpr ((Mode & 128) != 0) {
+    unsigned long long* o = reinterpret_cast<unsigned long long*>(const_cast<float*>(P.gain)) +
+                            (static_cast<size_t>(blockIdx.x) * 4 + wave) * 4;
+    if (lane == 0) {
+      o[0] = st_w;
+      o[1] = st_m;
+      o[2] = st_s;
+      o[3] = st_b;
+    }
+  }
+}
+
+// ---- config 4's shape with 64-beam waves (the default with a workspace there) ------------------------------------------
+// The 32-beam kernels run two workgroups per CU, one per slab, so every voltage byte reaches a CU twice (the second
+// slab's read from L2), and the halved-image form above holds 256 VGPRs, which leaves no room to fetch the step's
+// LDS fragments ahead of its MFMAs (steps at ~45 % of the MFMA pipe).  Here a workgroup is 8 waves (two per SIMD)
+// over both slabs of a channel group: a wave owns 16 samples x all 64 beams x 2 pols (128 accumulator registers,
+// as before), each lane loads one 4-byte sample run per antenna (the same load instructions per MFMA as the 32-beam
+// kernels, each byte once per CU), and with ~100 registers to spare the step's 8 A fragments are read at its start,
+// a 4-step voltage ring stays in flight and y_im's fragments are built once per step (24 VALU per 32 MFMAs).  The two
+// slabs' halved images (q14_image_kernel items) are LDS-DMA'd per channel into one of two 66 KiB buffers, slab p's
+// during pass p of the previous channel.  Shape: M = 64, 224 < A <= 256, T = 256 (16 sample chunks: 2 passes of 8).
+constexpr int kW64Threads = 512;
+__shared__ __attribute__((aligned(16))) int4 w64h_img0[2 * kW32HItemWords / 4];
+__shared__ __attribute__((aligned(16))) int4 w64h_img1[2 * kW32HItemWords / 4];
+
+// One step's B fragments [x_re, x_im] per pol from one sample's 8 antenna dwords (unsigned: x - 128).
+template <bool Signed>
+__device__ __forceinline__ void w16_frags(const uint32_t (&d)[8], i32x4_t (&f)[2]) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    uint32_t w[4];
+#pragma unroll
+    for (int m2 = 0; m2 < 4; ++m2) {
+      uint32_t a = d[2 * m2], b = d[2 * m2 + 1];
+      if constexpr (!Signed) {
+        a ^= 0x80808080u;
+        b ^= 0x80808080u;
+      }
+      w[m2] = __builtin_amdgcn_perm(b, a, p ? kSelP1 : kSelP0);
+    }
+    f[p] = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]), static_cast<int>(w[3])};
+  }
+}
+
+// Mode (diagnostics only): 2 no MFMA (a cheap VALU sum instead), 4 no stores, 8 no voltage loads (register-made
+// samples), 32 no image DMA after channel 0.
+template <bool Signed, bool Pow2, int kCh = 16, int NB = 4, int Mode = 0>
+__global__ __launch_bounds__(kW64Threads, 1) void beamform_fused_i8_w64h_kernel(FusedArgs P) {
+  constexpr int Sp = 8, NP = 2;
+  static_assert(Sp % NB == 0, "ring aligned with the passes");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 4, tl = lane & 15;
+  const int C = P.C;
+  const int gpb = (C + kCh - 1) / kCh;  // channel groups per batch
+  const int grp = blockIdx.x;
+  if (grp >= P.B * gpb) return;
+  const int b = grp / gpb, c0 = (grp - b * gpb) * kCh;
+  const int nk = min(kCh, C - c0);
+  const size_t ant_stride = static_cast<size_t>(C) * P.T * 4;
+  const uint32_t ch_bytes = static_cast<uint32_t>(P.T) * 4;
+  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * C + c0) * static_cast<size_t>(P.T) * 4;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(P.table), 0, 0x7fffffff,
+                                                                        0x00020000);
+  const uint32_t titem = static_cast<uint32_t>((b * C + c0) * 2 * kW32HItemWords * 4);  // (b, c0, slab 0)
+  const uint32_t tch = static_cast<uint32_t>(2 * kW32HItemWords * 4);                   // bytes per channel
+  const uint32_t lvoff = 16u * static_cast<uint32_t>(lane);
+  // slab sl's item of channel kc -> half sl of image buffer img: 4 of its 32 image KiB per wave, and a quarter of
+  // its 1 KiB column-sum block (waves w and w + 4 copy the same quarter)
+  auto dma_slab = [&](int kc, int4* img, int sl) {
+    const uint32_t src = titem + static_cast<uint32_t>(kc) * tch + static_cast<uint32_t>(sl * kW32HItemWords * 4);
+    int4* dst = img + sl * (kW32HItemWords / 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pc = wave_u + 8 * k;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void_ptr)(dst + 64 * pc), 16, lvoff,
+                                               src + 1024u * static_cast<uint32_t>(pc), 0, 0);
+    }
+    const int cs = 8192 + 64 * (wave_u & 3);  // words
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void_ptr)(reinterpret_cast<int*>(dst) + cs), 4, lvoff >> 2,
+                                             src + 4u * static_cast<uint32_t>(cs), 0, 0);
+  };
+
+  const int total = nk * NP * Sp;
+  int issued = 0, ls = 0, lp = 0, lk = 0;
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7fffffff,
+                                                                        0x00020000);
+  // lane (tl, h): sample tl of the wave's 16, antennas 8 h + q of the step; the rest of the offset is uniform
+  const uint32_t lvo = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride) + 4u * static_cast<uint32_t>(tl);
+  auto issue = [&](uint32_t (&d)[8]) {
+    const uint32_t sbase = static_cast<uint32_t>(w8_step_base(ls, P.A)) * static_cast<uint32_t>(ant_stride) +
+                           static_cast<uint32_t>(lk) * ch_bytes + static_cast<uint32_t>(wave_u + 8 * lp) * 64u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if constexpr ((Mode & 8) != 0) {
+        d[q] = lvo * 0x01010101u + sbase + q;
+        continue;
+      }
+      d[q] = __builtin_amdgcn_raw_buffer_load_b32(vrs, lvo, sbase + static_cast<uint32_t>(q) * static_cast<uint32_t>(ant_stride), 0);
+    }
+    ++issued;
+    const bool adv = issued < total;
+    const bool wrap = ls + 1 == Sp, pwrap = lp + 1 == NP;
+    ls = adv ? (wrap ? 0 : ls + 1) : ls;
+    lp = (adv && wrap) ? (pwrap ? 0 : lp + 1) : lp;
+    lk = (adv && wrap && pwrap) ? lk + 1 : lk;
+  };
+  uint32_t db[NB][8];
+  dma_slab(0, w64h_img0, 0);
+  dma_slab(0, w64h_img0, 1);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) issue(db[j]);
+  if constexpr (NB == 4) {
+    __builtin_amdgcn_s_waitcnt(0x8f70);  // vmcnt(32): the image DMAs (all but the 32 voltage loads after them)
+  } else {
+    static_assert(NB == 2, "ring depth");
+    __builtin_amdgcn_s_waitcnt(0x4f70);  // vmcnt(16)
+  }
+  lds_barrier();
+
+  const float s32 = P.out_scale * 0x1p-14f;
+  const int M2 = 2 * P.M;  // 128
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(P.y, 0, 0x7fffffff, 0x00020000);
+  const uint32_t so_lane = static_cast<uint32_t>(tl * M2 + 16 * (h >> 1) + 32 * (h & 1));
+  // Mode 64: the next channel's slab through registers instead of LDS-DMA -- 4 x 16-byte loads + 1 dword per lane at
+  // step 1 of a pass, written to LDS at step 5 (the DMA's issue cost measured ~60 us per launch at config 4)
+  u32x4_t tq[4];
+  uint32_t tcs = 0;
+  auto table_load = [&](int kc, int sl) {
+    const uint32_t src = titem + static_cast<uint32_t>(kc) * tch + static_cast<uint32_t>(sl * kW32HItemWords * 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      tq[k] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                             trs, lvoff, src + 1024u * static_cast<uint32_t>(wave_u + 8 * k), 0));
+    tcs = __builtin_amdgcn_raw_buffer_load_b32(trs, lvoff >> 2, src + 4u * static_cast<uint32_t>(8192 + 64 * (wave_u & 3)), 0);
+  };
+  auto table_store = [&](int4* img, int sl) {
+    int4* dst = img + sl * (kW32HItemWords / 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[64 * (wave_u + 8 * k) + lane] = __builtin_bit_cast(int4, tq[k]);
+    reinterpret_cast<uint32_t*>(dst)[8192 + 64 * (wave_u & 3) + lane] = tcs;
+  };
+  auto channel = [&](int kc, int4* img, int4* nxt) {
+    const int c = c0 + kc;
+    const int knext = min(kc + 1, nk - 1);
+#pragma unroll 1
+    for (int pass = 0; pass < NP; ++pass) {
+      i32x4_t rh[2][4], rl[2][4], ih[2][4], il[2][4];  // [pol][tile of 16 beams]
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) rh[p][t] = rl[p][t] = ih[p][t] = il[p][t] = i32x4_t{0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < Sp; ++s) {
+        const int j = s % NB;  // (Sp * pass is a multiple of NB)
+        // the step's A fragments first: their LDS latency runs under the fragment VALU and the ring refill
+        i32x4_t ahi[4], alo[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int4* im = img + (t >> 1) * (kW32HItemWords / 4);
+          const int4 x0 = im[((s * 2 + (t & 1)) * 2 + 0) * 64 + lane];
+          const int4 x1 = im[((s * 2 + (t & 1)) * 2 + 1) * 64 + lane];
+          ahi[t] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
+          alo[t] = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+        }
+        i32x4_t f[2], fi[2];
+        w16_frags<Signed>(db[j], f);
+        fi[0] = frag_im(f[0]);
+        fi[1] = frag_im(f[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(db[j]);
+        if constexpr ((Mode & 64) != 0) {
+          if (s == 1) table_load(knext, pass);
+          if (s == 5) table_store(nxt, pass);
+        } else if ((Mode & 32) == 0 && s == 1) {
+          dma_slab(knext, nxt, pass);  // slab `pass` of the next channel
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            if constexpr ((Mode & 2) != 0) {
+              rh[p][t] += ahi[t] + f[p];
+              rl[p][t] += alo[t] ^ fi[p];
+              continue;
+            }
+            rh[p][t] = mfma_i8(ahi[t], f[p], rh[p][t]);
+            rl[p][t] = mfma_i8(alo[t], f[p], rl[p][t]);
+            ih[p][t] = mfma_i8(ahi[t], fi[p], ih[p][t]);
+            il[p][t] = mfma_i8(alo[t], fi[p], il[p][t]);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // requantise + store: per pol two 16-byte row pieces, one per slab (tiles 2 sl, 2 sl + 1)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const size_t prow = ((static_cast<size_t>(b) * 2 + p) * C + c) * static_cast<size_t>(P.T);
+        const uint32_t srow = static_cast<uint32_t>((prow + 16 * (wave_u + 8 * pass)) * M2);
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          const int* csums = reinterpret_cast<const int*>(img + sl * (kW32HItemWords / 4)) + 8192;
+          uint32_t pk[2][2];  // [tile of the slab][dword]
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) {
+            const int t = 2 * sl + tt;
+            const int4 q0 = *reinterpret_cast<const int4*>(csums + 2 * (16 * tt + 4 * h));
+            const int4 q1 = *reinterpret_cast<const int4*>(csums + 2 * (16 * tt + 4 * h) + 4);
+            const int wc[4] = {q0.x, q0.z, q1.x, q1.z}, ws[4] = {q0.y, q0.w, q1.y, q1.w};
+            uint32_t qr[4], qi[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int cre = Signed ? 0 : 128 * (wc[r] - ws[r]);
+              const int cim = Signed ? -ws[r] : 128 * (wc[r] + ws[r]) - ws[r];
+              qr[r] = requant_bits<Pow2>((rh[p][t][r] << 8) + rl[p][t][r] + cre, s32);
+              qi[r] = requant_bits<Pow2>((ih[p][t][r] << 8) + il[p][t][r] + cim, s32);
+            }
+            pk[tt][0] = pack_low_bytes(qr[0], qi[0], qr[1], qi[1]);
+            pk[tt][1] = pack_low_bytes(qr[2], qi[2], qr[3], qi[3]);
+          }
+          const auto sw0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+          const auto sw1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+          if constexpr ((Mode & 4) != 0) {  // keep the values live, store almost nothing
+            if ((sw0[0] ^ sw1[1]) == 0x12345678u)
+              reinterpret_cast<uint32_t*>(P.y)[tid] = sw0[1] + sw1[0];
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u32x4_t{sw0[0], sw1[0], sw0[1], sw1[1]}),
+                                                   yrs, so_lane, srow + static_cast<uint32_t>(64 * sl), 0);
+          }
+        }
+      }
+    }
+    // this wave's DMA into `nxt` (the last at pass 1 step 1) has landed: all but the 6 x 8 later refills and the 4
+    // stores of pass 1
+    if constexpr ((Mode & 64) == 0) asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
+    lds_barrier();  // every wave is done with `img`; `nxt` is complete
+  };
+  for (int kc = 0; kc < nk; kc += 2) {  // (two copies of the body: each reads one buffer, DMAs into the other)
+    channel(kc, w64h_img0, w64h_img1);
+    if (kc + 1 < nk) channel(kc + 1, w64h_img1, w64h_img0);
+  }
+}
+
 template <bool Signed, int Mode>
 int launch_w32t_contract(FusedArgs P, hipStream_t st);
 #ifdef BF_DIAG
 template <bool Signed, int Mode>
 int launch_w32_overlapped(FusedArgs P, int k, hipStream_t st);
 #endif
+
+// The halved-image kernel's shape (beamform_fused_i8_w32h_kernel): 8 k-steps, T = 256, whole 32-beam slabs, every
+// in-workgroup voltage offset below 2^31, a whole launch (no channel chunk).
+bool w32h_fits(const FusedArgs& P) {
+  return w32_steps(P.A) == 8 && P.A > 224 && P.T == 256 && P.M % kW32Beams == 0 && P.c_count == 0 &&
+         static_cast<unsigned long long>(P.A) * P.C * P.T * 4 < (1ull << 31) &&
+         static_cast<unsigned long long>(P.B) * 2 * P.C * P.T * 2 * P.M < (1ull << 31) &&
+         w32_table_bytes(P.B, P.C, P.A, P.M) < (1ull << 31);
+}
+
+// config 4's exact shape for the one-wave-per-SIMD kernel (beamform_fused_i8_w64h_kernel)
+bool w64h_fits(const FusedArgs& P) { return w32h_fits(P) && P.M == 64; }
+
+template <bool Signed, int kCh = 16, int NB = 4, int Mode = 0>
+int launch_w64h_contract(FusedArgs P, hipStream_t st) {
+  const long long grid = static_cast<long long>(P.B) * ((P.C + kCh - 1) / kCh);
+  BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
+  if (scale_is_pow2(P.out_scale * 0x1p-14f))
+    hipLaunchKernelGGL((beamform_fused_i8_w64h_kernel<Signed, true, kCh, NB, Mode>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW64Threads), 0, st, P);
+  else
+    hipLaunchKernelGGL((beamform_fused_i8_w64h_kernel<Signed, false, kCh, NB, Mode>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW64Threads), 0, st, P);
+  BF_LAUNCHED("beamform_fused_i8_w64h_kernel");
+}
+
+// The halved-image contraction of one launch whose kLayoutW32H table is ready in P.table on `st`.
+template <bool Signed, int Mode = 0>
+int launch_w32h_contract(FusedArgs P, hipStream_t st) {
+  const size_t lds = 0;  // (static: the two image buffers)
+  const long long groups = static_cast<long long>(P.B) * ((P.C + kW32HChannels - 1) / kW32HChannels);
+  const long long grid = P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs;
+  BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
+  if (scale_is_pow2(P.out_scale * 0x1p-14f))
+    hipLaunchKernelGGL((beamform_fused_i8_w32h_kernel<Signed, true, Mode>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW8Threads), lds, st, P);
+  else
+    hipLaunchKernelGGL((beamform_fused_i8_w32h_kernel<Signed, false, Mode>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW8Threads), lds, st, P);
+  BF_LAUNCHED("beamform_fused_i8_w32h_kernel");
+}
 
 template <bool Signed, int Mode = 0>
 int launch_w32(FusedArgs P, hipStream_t st) {
@@ -1087,6 +1624,15 @@ int launch_w32(FusedArgs P, hipStream_t st) {
     const int nover = ov ? std::min(16, std::max(1, atoi(ov))) : 1;
     if (nover > 1 && P.B == 1 && P.c_count == 0 && P.delay_channels == 1)
       return launch_w32_overlapped<Signed, Mode>(P, nover, st);
+#endif
+#ifdef BF_DIAG
+    // measurement (BF_W32H=1 / BF_W64H=1): the halved-image generator + the w32h or w64h contraction at config 4's
+    // shape -- bitwise equal to the table kernel, measured no faster (profiles/r4_*)
+    if (Mode == 0 && w32h_fits(P) && (diag_env("BF_W32H") || (diag_env("BF_W64H") && w64h_fits(P)))) {
+      const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32H, st);
+      if (e != BF_OK) return e;
+      return diag_env("BF_W64H") ? launch_w64h_contract<Signed, 16, 2>(P, st) : launch_w32h_contract<Signed>(P, st);
+    }
 #endif
     const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32, st);
     if (e != BF_OK) return e;
@@ -1238,7 +1784,35 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   P.nslabs = (M + 31) / 32;
   P.xcd_order = P.nslabs > 1;
   hipStream_t st = bf::as_stream(stream);
+  if (mode == -2) return bf::launch_q14_table(P, static_cast<uint32_t*>(table), bf::kLayoutW32H, st);
   if (mode < 0) return bf::launch_q14_table(P, static_cast<uint32_t*>(table), bf::kLayoutW32, st);
+  if (mode >= 1200 && mode < 1300) {  // the one-wave-per-SIMD contraction alone: kCh 16 / 8, NB 4 / 2
+    switch (mode) {
+      case 1200: return bf::launch_w64h_contract<true, 16, 4>(P, st);
+      case 1201: return bf::launch_w64h_contract<true, 8, 4>(P, st);
+      case 1202: return bf::launch_w64h_contract<true, 16, 2>(P, st);
+      case 1210: return bf::launch_w64h_contract<true, 16, 4, 2>(P, st);
+      case 1211: return bf::launch_w64h_contract<true, 16, 4, 4>(P, st);
+      case 1212: return bf::launch_w64h_contract<true, 16, 4, 8>(P, st);
+      case 1213: return bf::launch_w64h_contract<true, 16, 4, 12>(P, st);
+      case 1214: return bf::launch_w64h_contract<true, 16, 4, 6>(P, st);
+      case 1215: return bf::launch_w64h_contract<true, 16, 4, 32>(P, st);
+      case 1216: return bf::launch_w64h_contract<true, 16, 4, 14>(P, st);
+      case 1220: return bf::launch_w64h_contract<true, 16, 2, 64>(P, st);
+      case 1221: return bf::launch_w64h_contract<true, 16, 4, 64>(P, st);
+      case 1222: return bf::launch_w64h_contract<true, 16, 2, 32>(P, st);
+      default: return BF_ERR_ARG;
+    }
+  }
+  if (mode >= 960 && mode < 1200) {  // the halved-image contraction alone (a kLayoutW32H table in `table`); +Mode bits
+    P.nslabs = (M + 31) / 32;
+    P.xcd_order = P.nslabs > 1;
+    switch (mode - 960) {
+      case 0: return bf::launch_w32h_contract<true, 0>(P, st);
+      case 16: return bf::launch_w32h_contract<true, 16>(P, st);
+      default: return BF_ERR_ARG;  // (Mode 128 needs a stamps buffer: bf_diag_w32h_stamps)
+    }
+  }
   const long long groups = static_cast<long long>(B) * ((C + bf::kW32TChannels - 1) / bf::kW32TChannels);
   const unsigned grid = static_cast<unsigned>(P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs);
   const size_t lds = bf::w32_lds_bytes(A);
@@ -1263,12 +1837,27 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   case 940 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8, false, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break
   switch (mode) {
     BF_W32T(0); BF_W32T(1); BF_W32T(4); BF_W32T(8); BF_W32T(9); BF_W32T(12);
-    BF_W32TB(0); BF_W32TB(1); BF_W32TB(4); BF_W32TB(8); BF_W32TB(9); BF_W32TB(12);
+    BF_W32TB(0); BF_W32TB(1); BF_W32TB(4); BF_W32TB(8); BF_W32TB(9); BF_W32TB(12); BF_W32TB(16); BF_W32TB(17);
     default: return BF_ERR_ARG;
   }
 #undef BF_W32TB
 #undef BF_W32T
   BF_LAUNCHED("beamform_fused_i8_w32t_kernel");
+}
+
+// The halved-image contraction with per-wave phase stamps (Mode 128): uint64 [grid][4 waves][4] -> stamps.
+extern "C" int bf_diag_w32h_stamps(const uint8_t* raw, const void* table, void* y, void* stamps, int B, int C, int T,
+                                   int A, int M, void* stream) {
+  bf::FusedArgs P{};
+  P.raw = raw;
+  P.y = y;
+  P.table = static_cast<const uint32_t*>(table);
+  P.gain = static_cast<const float*>(stamps);
+  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
+  P.out_scale = 1.0f / 64;
+  P.nslabs = (M + 31) / 32;
+  P.xcd_order = P.nslabs > 1;
+  return bf::launch_w32h_contract<true, 128>(P, bf::as_stream(stream));
 }
 
 // The whole table-driven launch (generator + contraction, as bf_beamform_fused_ws runs it); BF_W32_CHUNKS splits it
