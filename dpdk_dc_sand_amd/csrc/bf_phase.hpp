@@ -168,15 +168,9 @@ __device__ __forceinline__ int q14_pair_unit(double v, bool* ok) {
 }
 
 // q14_pair_unit on t = 2^14 v given directly (a recurrence kept in the 2^14-scaled domain: no rescale per value).
-// The common case is decided in float32: |t| <= 16384 (1 + 2^-40), so RN32(t) is within 2^-10 of t and
-// |RN32(t) - rint(RN32(t))| < kQ14UnitMargin - 2^-10 implies |t - n| < kQ14UnitMargin for n = rint(RN32(t)) (the
-// float32 difference is exact); one float64 conversion and three float32 operations where the float64 test took
-// four float64 operations (half rate).  The ~0.4 % of values it leaves undecided take the float64 path.
-constexpr float kQ14UnitMarginF32 = static_cast<float>(kQ14UnitMargin - 0x1p-10 - 0x1p-20);  // (rounded below the bound)
+// (A float32 first test -- RN32(t) within 2^-10 of t -- measured slower, 74.5 vs 62 us for the config-4 generator:
+// the ~0.4 % of values it leaves undecided put ~1 in 4 waves through both tests, profiles/r4_m_*.)
 __device__ __forceinline__ int q14_pair_unit_scaled(double t, bool* ok) {
-  const float tf = static_cast<float>(t);
-  const float nf = __builtin_rintf(tf);
-  if (fabsf(tf - nf) < kQ14UnitMarginF32) return static_cast<int>(nf);
   const double n = rint(t);
   if (fabs(t - n) < kQ14UnitMargin) return static_cast<int>(n);
   return q14_pair(t * 0x1p-14, 16384.0f, ok);

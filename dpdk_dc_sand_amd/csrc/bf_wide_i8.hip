@@ -832,6 +832,10 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
   const int b = grp / gpb, c0 = (grp - b * gpb) * kCh;
   const int nk = min(kCh, Cn - c0);
   const int m0 = slab * kW32Beams;
+#ifdef BF_DIAG
+  // measurement: static priority 1 for the workgroups with blockIdx bit (knob >> 8) set (knob & 1)
+  if ((P.knob & 1) && ((blockIdx.x >> (P.knob >> 8)) & 1)) __builtin_amdgcn_s_setprio(1);
+#endif
   const int Sp = kSp ? kSp : w32_steps(P.A);
   const int T2 = P.T >> 1;
   const int nchunks = (T2 + 15) >> 4;                      // 32-sample chunks
@@ -1356,6 +1360,9 @@ __global__ __launch_bounds__(kW64Threads, 1) void beamform_fused_i8_w64h_kernel(
   if (grp >= P.B * gpb) return;
   const int b = grp / gpb, c0 = (grp - b * gpb) * kCh;
   const int nk = min(kCh, C - c0);
+#ifdef BF_DIAG
+  if ((P.knob & 2) && wave >= 4) __builtin_amdgcn_s_setprio(1);  // measurement: the second-dispatched half first
+#endif
   const size_t ant_stride = static_cast<size_t>(C) * P.T * 4;
   const uint32_t ch_bytes = static_cast<uint32_t>(P.T) * 4;
   const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * C + c0) * static_cast<size_t>(P.T) * 4;
@@ -1784,6 +1791,7 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   P.nslabs = (M + 31) / 32;
   P.xcd_order = P.nslabs > 1;
   hipStream_t st = bf::as_stream(stream);
+  if (const char* kb = bf::diag_env("BF_KNOB")) P.knob = atoi(kb);  // measurement knobs (bf_fused.hpp)
   if (mode == -2) return bf::launch_q14_table(P, static_cast<uint32_t*>(table), bf::kLayoutW32H, st);
   if (mode < 0) return bf::launch_q14_table(P, static_cast<uint32_t*>(table), bf::kLayoutW32, st);
   if (mode >= 1200 && mode < 1300) {  // the one-wave-per-SIMD contraction alone: kCh 16 / 8, NB 4 / 2

@@ -67,6 +67,23 @@ def launch(i, form):
     assert e == 0, lib.bf_last_error()
 
 
+def timeit_mode(mode, n=20):
+    def run(i):
+        tbl = tbh.ptr if mode == -2 or mode >= 960 else tb.ptr
+        assert lib.bf_diag_w32_table(mode, xs[i % 2].ptr, dv.ptr, ys[i % 2].ptr, tbl, B, C, T, A, M, Ctot, 1 / 1712e6,
+                                     q.handle) == 0
+    for i in range(3):
+        run(i)
+    e0, e1 = accel.Event(), accel.Event()
+    q.finish()
+    e0.record(q)
+    for i in range(n):
+        run(i)
+    e1.record(q)
+    q.finish()
+    return e1.time_since(e0) / n
+
+
 def timeit(form, n=20):
     for i in range(3):
         launch(i, form)
@@ -128,3 +145,16 @@ tot = v.sum(axis=2)
 print(f"stamps over {v.shape[0]} workgroups x 4 waves (cycles per wave, mean): " + ", ".join(
     f"{n} {v[..., k].mean():.0f} ({100 * v[..., k].sum() / tot.sum():.1f} %)" for k, n in
     enumerate(("voltage wait", "steps (MFMA + LDS)", "requant + stores", "channel barrier"))))
+
+# static-priority knobs (BF_KNOB): 1 | bit << 8 = prio 1 for w32t workgroups with that blockIdx bit; 2 = w64h waves 4-7
+if os.environ.get("KNOB_AB"):
+    kres = {}
+    for r in range(5):
+        for name, mode, knob in (("w32t", 900, 0), ("w32t prio bit3", 900, 1 | 3 << 8), ("w32t prio bit8", 900, 1 | 8 << 8),
+                                 ("w32t prio bit0", 900, 1), ("w64h NB2", 1202, 0), ("w64h NB2 prio 4-7", 1202, 2)):
+            os.environ["BF_KNOB"] = str(knob)
+            kres.setdefault(name, []).append(timeit_mode(mode))
+    os.environ.pop("BF_KNOB", None)
+    for name, ts in kres.items():
+        ts = sorted(ts)
+        print(f"  knob {name:24s}: median {ts[len(ts) // 2] * 1e6:8.1f} us")
