@@ -506,6 +506,35 @@ __device__ __forceinline__ void w32_mfma(const int4* __restrict__ fr, int s, int
   }
 }
 
+// The same 32 MFMAs with the next tile's two A fragments read from LDS while the current tile's MFMAs issue (two
+// register sets): the single-set form made the compiler issue each tile's reads one MFMA before their use, so every
+// step waited out the LDS latency four times (ISA: s_waitcnt lgkmcnt(1) between the MFMAs of consecutive tiles).
+template <int Mode>
+__device__ __forceinline__ void w32_mfma_pf(const int4* __restrict__ fr, int s, int lane, const i32x4_t (&f)[2][2],
+                                            i32x4_t (&hi)[2][2][4], i32x4_t (&lo)[2][2][4]) {
+  int4 a[2][2];  // [register set][limb]
+  a[0][0] = fr[((s * 4 + 0) * 2 + 0) * 64 + lane];
+  a[0][1] = fr[((s * 4 + 0) * 2 + 1) * 64 + lane];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t + 1 < 4) {
+      a[(t + 1) & 1][0] = fr[((s * 4 + t + 1) * 2 + 0) * 64 + lane];
+      a[(t + 1) & 1][1] = fr[((s * 4 + t + 1) * 2 + 1) * 64 + lane];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // (else the scheduler sinks the reads back to one MFMA before their use)
+    const int4 x0 = a[t & 1][0], x1 = a[t & 1][1];
+    const i32x4_t chi = i32x4_t{x0.x, x0.y, x0.z, x0.w}, clo = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        hi[p][i][t] = mfma_i8(chi, f[p][i], hi[p][i][t]);
+        lo[p][i][t] = mfma_i8(clo, f[p][i], lo[p][i][t]);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads, 64 model loads
 // without the phasor math, 256 the phasor math on register-made delays (no model loads).
 template <bool Signed, int Mode = 0, bool Gain = false>
@@ -959,7 +988,10 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
           if constexpr ((Mode & 16) != 0) w32_frags_im(db[j], fi);
           __builtin_amdgcn_sched_barrier(0);
           issue(db[j]);
-          w32_mfma<Mode & 16>(lds4, s, lane, f, hi, lo, fi);
+          if constexpr ((Mode & 32) != 0)
+            w32_mfma_pf<0>(lds4, s, lane, f, hi, lo);
+          else
+            w32_mfma<Mode & 16>(lds4, s, lane, f, hi, lo, fi);
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
@@ -1846,6 +1878,10 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
   switch (mode) {
     BF_W32T(0); BF_W32T(1); BF_W32T(4); BF_W32T(8); BF_W32T(9); BF_W32T(12);
     BF_W32TB(0); BF_W32TB(1); BF_W32TB(4); BF_W32TB(8); BF_W32TB(9); BF_W32TB(12); BF_W32TB(16); BF_W32TB(17);
+#define BF_W32TP(m) \
+  case 1500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8, true, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break
+    BF_W32TP(32); BF_W32TP(33); BF_W32TP(36); BF_W32TP(40);
+#undef BF_W32TP
     default: return BF_ERR_ARG;
   }
 #undef BF_W32TB

@@ -158,3 +158,4 @@ if os.environ.get("KNOB_AB"):
     for name, ts in kres.items():
         ts = sorted(ts)
         print(f"  knob {name:24s}: median {ts[len(ts) // 2] * 1e6:8.1f} us")
+
