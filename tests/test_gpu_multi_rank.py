@@ -145,6 +145,31 @@ def test_bench_rccl_scatter_path_one_rank(tmp_path):
     assert line["value"] > 0
 
 
+def _visible_devices():
+    import torch  # device_count() does not initialise the GPU on this image
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_visible_devices() < 2, reason="the RCCL channel scatter across ranks needs two GPUs")
+def test_bench_rccl_scatter_two_ranks(tmp_path):
+    """bench.py --gpus 2 over RCCL (one rank per GPU): the root's band is packed and sent to both ranks, and every
+    rank's received slice is checksummed on its device and compared with the root's band slice [C r, C (r + 1))."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--settle-ms", "0", "--scatter-backend", "rccl", "--workload", "cfg2", "--no-secondary",
+           "--no-pmc", "--no-cpu-baseline", "--no-ceiling", "--no-rocprof"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    sc = line["scatter"]
+    assert "error" not in sc and sc["backend"] == "rccl" and sc["ranks"] == 2, sc
+    assert line["scatter_ok"] is True and sc["verified"] is True, sc
+    assert [c["match"] for c in sc["checksums"]] == [True, True], sc
+
+
 def test_channel_scatter_one_rank_comm():
     """libbf's communicator at one rank: the RCCL id, bf_comm_create, bf_comm_allreduce_max (an RCCL all-reduce) and
     bf_channel_scatter of a (B, A, C, T, 2, 2) band into a slice (the root's own 2-D pack) equal the numpy slice; the

@@ -59,15 +59,16 @@ ROUNDS = int(_os.environ.get("DIAG_ROUNDS", "1"))
 if "wide" in _os.environ.get("DIAG_KERNELS", ""):
     lib.bf_diag_wide.argtypes = [I, I, V, V, V, I, I, I, I, I, I, D, V]
     wnames = {0: "full (fast coef)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 8: "no-load", 3: "no-coef,no-mfma",
-              5: "no-coef,no-store", 16: "nt stores", 32: "branchy phasor validity", 64: "hw sin/cos phasors",
+              5: "no-coef,no-store", 16: "nt stores", 32: "branchy phasor validity", 64: "round-3 polynomial phasors",
               1000: "buffer loads", 1001: "buffer loads, no-coef", 1004: "buffer loads, no-store",
-              1064: "buffer loads, hw sin/cos phasors"}
+              1064: "buffer loads, round-3 polynomial phasors", 128: "round-3 pair index math",
+              1128: "buffer loads, round-3 pair index math"}
     if _os.environ.get("WIDE_MODES"):
         wnames = {int(m): wnames.get(int(m), str(m)) for m in _os.environ["WIDE_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
     for tw in [int(t) for t in _os.environ.get("WIDE_TW", "2,1").split(",")]:
         ref = None
-        for mode in [m for m in wnames if m % 1000 in (0, 64)]:  # float beams of the full forms against mode 0
+        for mode in [m for m in wnames if m % 1000 in (0, 64, 128)]:  # float beams of the full forms against mode 0
             assert lib.bf_diag_wide(mode, tw, bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, B, C, T, A, M, Ctot, 1 / 1712e6,
                                     q.handle) == 0
             y = bufs[0][1].get(q).view(np.float32).astype(np.float64)
