@@ -829,7 +829,8 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(Fu
 // walks kCh consecutive channels of its slab (kW32TChannels; 8 at config 4's shape): the next channel's table is
 // requested after the current channel's last MFMAs (its latency under the stores), and the voltage prefetch runs on
 // from one channel into the next, so only a workgroup's first channel starts cold (measured on the one-channel form: a cold start -- table +
-// first voltage steps -- per (channel, slab) cost ~50 us of 430 at config 4, profiles/r3_e_w32t_ablation.txt).
+// first voltage steps -- per (channel, slab) cost ~50 us of 430 at config 4 in a round-3 ablation whose record was
+// not kept).
 // Mode (diagnostics): 1 no table loads / expansion, 4 no stores, 8 no voltage loads.
 constexpr int kW32TChannels = 4;
 
