@@ -779,9 +779,9 @@ template <bool Signed>
 int dispatch_table(const uint8_t* x, const float* w, float* y, long long bpc, int NB, int A, int M, int S, int NT,
                    hipStream_t st) {
   const char* os = diag_env("BF_TABLE_OS");  // measurement: 0 keeps the slab kernels
-  // 4 waves per item (256 VGPRs, two workgroups per CU), spill-free in the one-loop form.  The 8-wave form (128
-  // VGPRs) ran 2 % faster in its peeled form (801 vs 819 us at config 4, profiles/r4_c_table_os_ab.txt) but spills
-  // 24-40 B/lane in either form; bounded to 3 waves per SIMD it fits, but one workgroup per CU runs 903 us
+  // 4 waves per item (256 VGPRs, two workgroups per CU), spill-free in the one-loop form: 791 us at config 4 against
+  // 853 for the 8-wave form (128 VGPRs, spills 24-40 B/lane) and 933 for the 8-wave form bounded to 3 waves per
+  // SIMD (no spill, one workgroup per CU), profiles/r4_s_table_os_ab.txt
   if (table_os_fits(NB, A, M, x, w) && !(os && os[0] == '0')) return launch_table_os<Signed, 0, 4>(x, w, y, bpc, A, st);
   // Long rows (>= 16 k-steps: 256+ antennas): the widest slab whose staged fragments leave room for a second
   // workgroup per CU, so one workgroup's table staging overlaps the other's contraction (cfg4: a 128 KiB slab held

@@ -1659,7 +1659,7 @@ int launch_w32(FusedArgs P, hipStream_t st) {
 #ifdef BF_DIAG
     // measurement (BF_W32_OVERLAP = k chunks): the generator's chunks on a second stream, each chunk's contraction
     // on the caller's stream after its chunk of the table.  Measured slower than the serial pair (round 4,
-    // profiles/r4_c_w32_overlap_ab.txt: 2 / 4 / 8 chunks 493 / 518 / 852 vs 466 us), so diagnostic only.
+    // profiles/r4_s_overlap_ab.txt: 2 / 4 / 8 chunks 494 / 505 / 843 vs 478 us, bitwise equal), so diagnostic only.
     const char* ov = diag_env("BF_W32_OVERLAP");
     const int nover = ov ? std::min(16, std::max(1, atoi(ov))) : 1;
     if (nover > 1 && P.B == 1 && P.c_count == 0 && P.delay_channels == 1)
