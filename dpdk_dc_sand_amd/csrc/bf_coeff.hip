@@ -168,6 +168,43 @@ __global__ __launch_bounds__(256) void coeff_gen_time_kernel(const float4* __res
   }
 }
 
+// The C++ study's own time-dependent convention (calculate_beamweights_grouped_channels_and_timestamps,
+// BeamformerKernels.cu:155-170), restated operation for operation in float32: the delay RATE in the channel term and
+// the opposite sign of the Python path, dt = t * Ts * fft_size, precise sincosf (the reference's
+// __sincosf is its fast-math form; its own golden, BeamformerCoefficientTest.cu:294-337, uses cos / sin).  Delay
+// model [a * M + m] as 4 floats (delay_s, delay_rate, phase_rad, phase_rate) -- the study's struct delay_vals
+// (BeamformerParameters.h:61-66) with its antenna-major (a, beam) index -- output [t][c][a][m] complex.
+template <bool F16>
+__global__ __launch_bounds__(256) void coeff_gen_time_study_kernel(const float4* __restrict__ dv,
+                                                                   void* __restrict__ out, int n_times, int C, int A,
+                                                                   int M, float ts, int fft_size) {
+  const long long n = static_cast<long long>(n_times) * C * A * M;
+  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+  const float pi = 3.14159265358979323846f;
+  for (long long idx = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; idx < n; idx += stride) {
+#pragma clang fp contract(off)  // separate roundings, as the study's float expressions
+    const int am = static_cast<int>(idx % (static_cast<long long>(A) * M));
+    long long r = idx / (static_cast<long long>(A) * M);
+    const int c = static_cast<int>(r % C);
+    const int t = static_cast<int>(r / C);
+    const float4 d = dv[am];
+    const float delta_time = t * ts * fft_size;
+    const float delta_delay = d.y * delta_time;
+    const float delta_phase = d.w * delta_time;
+    const float delay_n2 = (d.x + delta_delay) * (C / 2) * pi / (ts * C);
+    const float delay_n = (d.y + delta_delay) * c * pi / (ts * C);
+    const float phase0 = d.z - delay_n2 + delta_phase;
+    const float rotation = delay_n + phase0;
+    float sn, cs;
+    sincosf(rotation, &sn, &cs);
+    if constexpr (F16) {
+      reinterpret_cast<__half2*>(out)[idx] = __floats2half2_rn(cs, sn);
+    } else {
+      reinterpret_cast<float2*>(out)[idx] = make_float2(cs, sn);
+    }
+  }
+}
+
 static int grid_for(long long n) {
   long long g = (n + 255) / 256;
   if (g > 256LL * 16) g = 256LL * 16;  // grid-stride beyond 16 blocks per CU
@@ -246,4 +283,21 @@ extern "C" int bf_coeff_gen_time(const float* delay_vals, int delay_channels, vo
                        static_cast<double>(Ctot), sample_period, t0, dt_step);
   }
   BF_LAUNCHED("coeff_gen_time_kernel");
+}
+
+extern "C" int bf_coeff_gen_time_study(const float* delay_vals, void* out, int out_fp16, int n_times, int C, int A,
+                                       int M, float sample_period, int fft_size, void* stream) {
+  BF_REQUIRE(delay_vals && out, "bf_coeff_gen_time_study: null pointer");
+  BF_REQUIRE(n_times > 0 && C > 0 && A > 0 && M > 0 && fft_size > 0, "bf_coeff_gen_time_study: bad shape");
+  BF_REQUIRE(sample_period > 0.0f, "bf_coeff_gen_time_study: sample_period must be > 0");
+  BF_REQUIRE((reinterpret_cast<uintptr_t>(delay_vals) & 15) == 0, "bf_coeff_gen_time_study: misaligned delay_vals");
+  const long long n = static_cast<long long>(n_times) * C * A * M;
+  const auto dv = reinterpret_cast<const float4*>(delay_vals);
+  if (out_fp16)
+    hipLaunchKernelGGL(bf::coeff_gen_time_study_kernel<true>, dim3(bf::grid_for(n)), dim3(256), 0,
+                       bf::as_stream(stream), dv, out, n_times, C, A, M, sample_period, fft_size);
+  else
+    hipLaunchKernelGGL(bf::coeff_gen_time_study_kernel<false>, dim3(bf::grid_for(n)), dim3(256), 0,
+                       bf::as_stream(stream), dv, out, n_times, C, A, M, sample_period, fft_size);
+  BF_LAUNCHED("coeff_gen_time_study_kernel");
 }

@@ -89,6 +89,18 @@ int bf_coeff_gen_time(const float* delay_vals, int delay_channels, void* out, in
                       int C, int Ctot, int A, int M, int xeng_id, double sample_period, double t0,
                       double dt_step, void* stream);
 
+/* Time-dependent coefficients in the C++ study's OWN convention (replaces
+ * calculate_beamweights_grouped_channels_and_timestamps, BeamformerKernels.cu:121-189, formula :155-170):
+ *   dt = t*Ts*fft_size, dd = delay_rate*dt,
+ *   rot = (delay_rate + dd)*c*pi/(Ts*C) + phase - (delay + dd)*(C/2)*pi/(Ts*C) + phase_rate*dt   (float32),
+ * i.e. the delay rate in the channel term and the sign opposite to the Python path -- kept so that a
+ * caller of the study's kernel gets its numbers; pinned by the study's own golden (BeamformerCoefficientTest.cu:
+ * 294-337, tolerance 1e-4) restated in oracle/.
+ *   delay_vals : f32 (A*M, 4), index a*M + m (the study's antenna-major struct delay_vals array)
+ *   out        : (n_times, C, A, M) complex: out_fp16 = 0 -> float2 (cos, sin); 1 -> half2 */
+int bf_coeff_gen_time_study(const float* delay_vals, void* out, int out_fp16, int n_times, int C, int A, int M,
+                            float sample_period, int fft_size, void* stream);
+
 /* Pre-beamform reorder, bit-exact.
  * Replaces PreBeamformReorder._run / prebeamform_reorder kernel (beamformer/beamforming/prebeamform_reorder.py:
  * 171-186, kernels/prebeamform_reorder_kernel.mako:37-93):

@@ -193,3 +193,49 @@ def fused_beamform_int8(raw, delay_vals, Ctot, xeng_id=0, Ts=TS_MEERKAT, t0=0.0,
     s = np.float32(np.float32(scale) * np.float32(2.0 ** -Q14))
     q = np.rint(Y.astype(np.float32) * s)
     return np.clip(q, -127, 127).astype(np.int8).reshape(B, 2, C, T // 16, 16, -1)
+
+
+# ---- the C++ study's time-dependent steering coefficients (beamformer_coefficient_generator/) -----------------
+STUDY_TS = np.float32(1e-7)  # SAMPLING_PERIOD 1e-7f (BeamformerParameters.h:14)
+STUDY_FFT = 8192  # FFT_SIZE (BeamformerParameters.h:15)
+
+
+def study_delay_ramp(A, M, Ts=STUDY_TS):
+    """The study harness's delay model (BeamformerCoeffTest::simulate_input, BeamformerCoefficientTest.cu:185-196):
+    entry i of the A*M antenna-major array = (i/(A M) * Ts/3, 2e-6, (1 - i/(A M)) * Ts/3, 3e-6), float32."""
+    n = A * M
+    i = np.arange(n, dtype=np.float32)
+    d = np.empty((n, 4), np.float32)
+    # ((float)i / (float)n) * SAMPLING_PERIOD is float arithmetic; "/ 3.0" is double; the struct field is float
+    ts = np.float32(Ts)
+    d[:, 0] = ((i / np.float32(n)) * ts).astype(np.float64) / 3.0
+    d[:, 1] = np.float32(2e-6)
+    d[:, 2] = ((np.float32(1) - i / np.float32(n)) * ts).astype(np.float64) / 3.0
+    d[:, 3] = np.float32(3e-6)
+    return d
+
+
+def study_coeffs_time(delay_vals, n_times, C, A, M, Ts=STUDY_TS, fft_size=STUDY_FFT):
+    """The study's CPU golden for its time-dependent kernels (BeamformerCoeffTest::verify_output,
+    BeamformerCoefficientTest.cu:294-337), operation for operation:
+        timeStep_ns = long(float32(t * Ts * 1e9f * FFT));  dt = float32(timeStep_ns) / 1e9f       (:299, ts_diff :12-18)
+        dd = rate * dt;  delayN = (rate + dd) * c * pi / (Ts * C)                                   (float32, :321-322)
+        delayN2 = float32((delay + dd) * (C / 2.0) * pi / (Ts * C))   -- C / 2.0 is a double: double arithmetic (:323)
+        rot = delayN + (phase - delayN2 + phase_rate * dt);  (cos rot, sin rot)                     (:324-328)
+    delay_vals: (A*M, 4) float32, index a*M + m.  Returns complex64 (n_times, C, A, M)."""
+    f32 = np.float32
+    d = np.asarray(delay_vals, np.float32).reshape(A, M, 4)
+    delay, rate, phase, prate = (d[..., k][None, None] for k in range(4))
+    t = np.arange(n_times, dtype=np.float32)
+    step_ns = np.trunc(t * f32(Ts) * f32(1e9) * f32(fft_size)).astype(np.int64)
+    dt = (step_ns.astype(np.float32) / f32(1e9)).astype(np.float32)[:, None, None, None]
+    c = np.arange(C, dtype=np.float32)[None, :, None, None]
+    pi = f32(math.pi)
+    tsc = f32(f32(Ts) * f32(C))
+    dd = (rate * dt).astype(np.float32)
+    delay_n = ((((rate + dd) * c) * pi) / tsc).astype(np.float32)
+    delay_n2 = ((((delay + dd).astype(np.float64) * (C / 2.0)) * np.float64(pi)) / np.float64(tsc)).astype(np.float32)
+    dphase = (prate * dt).astype(np.float32)
+    phase0 = ((phase - delay_n2) + dphase).astype(np.float32)
+    rot = (delay_n + phase0).astype(np.float32).astype(np.float64)
+    return (np.cos(rot).astype(np.float32) + 1j * np.sin(rot).astype(np.float32)).astype(np.complex64)

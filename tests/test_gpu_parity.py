@@ -4,6 +4,8 @@ Mirrors the reference's four GPU unit tests (beamformer/unit_test/*_test.py) -- 
 (test_parameters.py), same input generators, same tolerances -- and adds what they mask:
 non-uniform per-(c, m, a) delays, xeng_id > 0, per-beam-varying coefficients, signed samples, odd shapes.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -182,6 +184,35 @@ def test_coeff_gen_time_matches_oracle(context, command_queue):
         np.testing.assert_array_equal(got[t, ..., 1], sin.transpose(0, 2, 1))
         np.testing.assert_array_equal(got16[t, ..., 0], cos.transpose(0, 2, 1).astype(np.float16))
         np.testing.assert_array_equal(got16[t, ..., 1], sin.transpose(0, 2, 1).astype(np.float16))
+
+
+@pytest.mark.parametrize("shape", [(256, 64, 64, 16), (3, 6, 5, 3)])
+def test_coeff_gen_time_study_matches_study_golden(context, command_queue, shape):
+    """The C++ study's own time-dependent convention (bf_coeff_gen_time_study, BeamformerKernels.cu:155-170) against
+    its harness's golden (BeamformerCoefficientTest.cu:294-337, restated in oracle.study_coeffs_time) on the
+    harness's delay ramp (simulate_input, :185-196) with nonzero delay and phase rates, at the study's default shape
+    (256 times x 64 channels x 64 antennas x 16 beams) and a ragged one.  Bar: the harness's own 1e-4 absolute
+    tolerance on every float (runBeamformerTests.cpp:30, verify_output :348-357); the half2 output (which the
+    harness does not check, :281-287) within half a float16 ulp of 1 plus the float bar."""
+    from dpdk_dc_sand_amd import accel
+    NT, C, A, M = shape
+    d = O.study_delay_ramp(A, M)
+    dv = accel.DeviceArray(context, d.shape, np.float32)
+    dv.set(command_queue, d)
+    out = accel.DeviceArray(context, (NT, C, A, M, 2), np.float32)
+    out16 = accel.DeviceArray(context, (NT, C, A, M, 2), np.float16)
+    _lib.call("bf_coeff_gen_time_study", dv.ptr, out.ptr, 0, NT, C, A, M, ctypes.c_float(1e-7), 8192,
+              command_queue.handle)
+    _lib.call("bf_coeff_gen_time_study", dv.ptr, out16.ptr, 1, NT, C, A, M, ctypes.c_float(1e-7), 8192,
+              command_queue.handle)
+    w = O.study_coeffs_time(d, NT, C, A, M)
+    ref = np.stack([w.real, w.imag], axis=-1)
+    got, got16 = out.get(command_queue), out16.get(command_queue).astype(np.float32)
+    assert np.abs(got - ref).max() <= 1e-4
+    assert np.abs(got16 - ref).max() <= 2 ** -11 + 1e-4
+    # the rates matter at this shape: the last time's phasors are far from the first's
+    if NT > 1:
+        assert np.abs(ref[-1] - ref[0]).max() > 0.5
 
 
 # ---- beamform multiply (beamform_mult_kernel_test.py:119-269: rtol = atol = 1e-4) -------------------------

@@ -141,3 +141,36 @@ def test_reference_bar_arbitration_path():
     bad.reshape(-1)[7] += 2.0  # farther from the exact product than the reference, outside the bar and the fp32 bound
     with pytest.raises(AssertionError):
         assert_reference_bar(bad, ref, x, w)
+
+
+def test_study_time_golden_restatement():
+    """oracle.study_coeffs_time (the C++ study's CPU golden, BeamformerCoefficientTest.cu:294-337, vectorised) equals
+    a scalar restatement of that loop, element by element in the golden's own float / double order, on the study's
+    delay ramp (simulate_input, :185-196) at a spread of (t, c, a, m) -- the study's dt != 0 convention."""
+    import math
+
+    f32, f64 = np.float32, np.float64
+    A, M, C, NT = 64, 16, 64, 256  # the study's defaults (BeamformerParameters.h:7-11)
+    d = O.study_delay_ramp(A, M)
+    assert d.dtype == np.float32 and d.shape == (A * M, 4)
+    # simulate_input's ramp, scalar: ((float)i / (float)n) * SAMPLING_PERIOD / 3.0
+    for i in (0, 1, 517, A * M - 1):
+        assert d[i, 0] == f32(f64(f32(f32(i) / f32(A * M)) * f32(1e-7)) / 3.0)
+        assert d[i, 2] == f32(f64(f32(f32(1) - f32(i) / f32(A * M)) * f32(1e-7)) / 3.0)
+    w = O.study_coeffs_time(d, NT, C, A, M)
+    assert w.shape == (NT, C, A, M) and w.dtype == np.complex64
+    ts, pi = f32(1e-7), f32(math.pi)
+    for t, c, a, m in ((0, 0, 0, 0), (1, 3, 5, 7), (17, 63, 0, 15), (128, 31, 40, 2), (255, 63, 63, 15)):
+        step = int(f32(f32(f32(t) * ts) * f32(1e9)) * f32(8192))  # long timeStep = t*SAMPLING_PERIOD*1e9f*FFT_SIZE
+        dt = f32(f32(step) / f32(1e9))  # ts_diff: (float) nanosec_difference / 1e9f
+        delay, rate, phase, prate = (f32(v) for v in d[a * M + m])
+        dd = f32(rate * dt)
+        delay_n = f32(f32(f32(f32(rate + dd) * f32(c)) * pi) / f32(ts * f32(C)))
+        delay_n2 = f32(f64(f32(delay + dd)) * (C / 2.0) * f64(pi) / f64(f32(ts * f32(C))))
+        rot = f32(delay_n + f32(f32(phase - delay_n2) + f32(prate * dt)))
+        assert w[t, c, a, m].real == f32(math.cos(rot)) and w[t, c, a, m].imag == f32(math.sin(rot)), (t, c, a, m)
+    # the convention differs from the Python path's (delay rate in the channel term, opposite sign): at t = 0 and
+    # c = 0 the study's phase is phase - delay * (C/2) * pi / (Ts C), the Python path's phase + pi * delay / (2 Ts)
+    assert np.allclose(np.angle(w[0, 0, :, :]).ravel(),
+                       np.angle(np.exp(1j * (d[:, 2].astype(np.float64) - d[:, 0] * (C / 2) * np.pi / (1e-7 * C)))),
+                       atol=1e-6)
