@@ -210,8 +210,8 @@ def test_coeff_gen_time_study_matches_study_golden(context, command_queue, shape
     got, got16 = out.get(command_queue), out16.get(command_queue).astype(np.float32)
     assert np.abs(got - ref).max() <= 1e-4
     assert np.abs(got16 - ref).max() <= 2 ** -11 + 1e-4
-    # the rates matter at this shape: the last time's phasors are far from the first's
-    if NT > 1:
+    # the rates matter at the study's shape: its last time's phasors are far from its first's
+    if NT >= 256:
         assert np.abs(ref[-1] - ref[0]).max() > 0.5
 
 
