@@ -60,6 +60,14 @@ def test_argument_validation_without_gpu():
         _lib.call("bf_beamform_fused", fake + 1, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0, 0, 1.0, None)
     with pytest.raises(_lib.BeamformerError, match="unknown flags"):
         _lib.call("bf_beamform_fused", fake, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0, 64, 1.0, None)
+    with pytest.raises(_lib.BeamformerError, match="null pointer"):
+        _lib.call("bf_coeff_gen_time_study", None, fake, 0, 4, 4, 4, 4, 1e-7, 8192, None)
+    with pytest.raises(_lib.BeamformerError, match="bad shape"):
+        _lib.call("bf_coeff_gen_time_study", fake, fake, 0, 0, 4, 4, 4, 1e-7, 8192, None)
+    with pytest.raises(_lib.BeamformerError, match="sample_period"):
+        _lib.call("bf_coeff_gen_time_study", fake, fake, 0, 4, 4, 4, 4, 0.0, 8192, None)
+    with pytest.raises(_lib.BeamformerError, match="misaligned"):
+        _lib.call("bf_coeff_gen_time_study", fake + 4, fake, 0, 4, 4, 4, 4, 1e-7, 8192, None)
 
 
 def test_algorithmic_bytes():

@@ -62,7 +62,8 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
               5: "no-coef,no-store", 16: "nt stores", 32: "branchy phasor validity", 64: "round-3 polynomial phasors",
               1000: "buffer loads", 1001: "buffer loads, no-coef", 1004: "buffer loads, no-store",
               1064: "buffer loads, round-3 polynomial phasors", 128: "round-3 pair index math",
-              1128: "buffer loads, round-3 pair index math"}
+              1128: "buffer loads, round-3 pair index math", 1256: "buffer loads, prio contraction",
+              1512: "buffer loads, prio phasors", 2024: "buffer loads, 16-pair model batches"}
     if _os.environ.get("WIDE_MODES"):
         wnames = {int(m): wnames.get(int(m), str(m)) for m in _os.environ["WIDE_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
