@@ -67,6 +67,7 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
     if _os.environ.get("WIDE_MODES"):
         wnames = {int(m): wnames.get(int(m), str(m)) for m in _os.environ["WIDE_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
+    ref0 = None  # the first form's beams: every later form (tw) is compared with it too (22: both slabs per workgroup)
     for tw in [int(t) for t in _os.environ.get("WIDE_TW", "2,1").split(",")]:
         ref = None
         for mode in [m for m in wnames if m % 1000 in (0, 64, 128)]:  # float beams of the full forms against mode 0
@@ -75,8 +76,10 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
             y = bufs[0][1].get(q).view(np.float32).astype(np.float64)
             if ref is None:
                 ref = y
+            if ref0 is None:
+                ref0 = y
             print(f"  wide tw={tw} mode {mode:4d} vs mode {min(wnames)}: max |dy| {np.abs(y - ref).max():.3e} "
-                  f"(max |y| {np.abs(ref).max():.3e})")
+                  f"(max |y| {np.abs(ref).max():.3e}); vs the first form: max |dy| {np.abs(y - ref0).max():.3e}")
         res = {m: [] for m in wnames}
         for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
             for mode in wnames:
