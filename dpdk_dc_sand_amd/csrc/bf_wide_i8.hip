@@ -429,7 +429,8 @@ __device__ __forceinline__ void w32_load_buf(__amdgpu_buffer_rsrc_t rs, uint32_t
       d[q] = u32x2_t{voff * 0x01010101u + sbase + q, voff * 0x01010101u + sbase - q};
       continue;
     }
-    d[q] = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, sbase + q * stride, 0));
+    // (Mode 128, diagnostics: non-temporal voltage loads)
+    d[q] = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, sbase + q * stride, (Mode & 128) ? 2 : 0));
   }
 }
 
@@ -916,7 +917,8 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
           tq[j][hf] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      rs, static_cast<uint32_t>(((min(j, Sp / 2 - 1) * 2 + hf) * 256 + tid) * 16), 0, 0));
+                                                      rs, static_cast<uint32_t>(((min(j, Sp / 2 - 1) * 2 + hf) * 256 + tid) * 16), 0,
+                                                      (Mode & 64) ? 2 : 0));  // (Mode 64, diagnostics: non-temporal)
     }
   };
   load_table(0);
@@ -1881,7 +1883,7 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
     BF_W32TB(0); BF_W32TB(1); BF_W32TB(4); BF_W32TB(8); BF_W32TB(9); BF_W32TB(12); BF_W32TB(16); BF_W32TB(17);
 #define BF_W32TP(m) \
   case 1500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8, true, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break
-    BF_W32TP(32); BF_W32TP(33); BF_W32TP(36); BF_W32TP(40);
+    BF_W32TP(32); BF_W32TP(33); BF_W32TP(36); BF_W32TP(40); BF_W32TP(64); BF_W32TP(128); BF_W32TP(192);
 #undef BF_W32TP
     default: return BF_ERR_ARG;
   }

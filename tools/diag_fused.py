@@ -112,6 +112,8 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
     # round 4: the next tile's A fragments read while the current tile's MFMAs issue (w32_mfma_pf)
     tnames.update({1532 + m: v.replace("early ", "") + " [NB2, 8 ch, buffer loads, A prefetch]" for m, v in base.items()
                    if m in (0, 1, 4, 8)})
+    tnames.update({1564: "full [NB2, 8 ch, buffer loads, nt table loads]", 1628: "full [NB2, 8 ch, buffer loads, nt voltage loads]",
+                   1692: "full [NB2, 8 ch, buffer loads, nt table + voltage loads]"})
     # 700 + m: the output-stationary LDS-DMA kernel (bf_wide_i8os.hip) on the same table; m = its Mode bits
     tnames.update({700 + m: v.replace("early ", "") + " [os, LDS-DMA]" for m, v in base.items() if m in (0, 1, 4, 8, 9, 12)})
     tnames.update({702: "no-mfma [os]", 705: "no table,no-store [os]",
@@ -133,7 +135,7 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
         if mode >= 0 and w32t_call(mode, 0) != 0:
             print(f"  w32t mode {mode}: launch failed: {lib.bf_last_error().decode(errors='replace')}")
             tnames.pop(mode)
-    for alt in (220, 240, 260, 280, 700, 900, 920, 940, 1532):  # another form's int8 beams, same input and table: bitwise equal
+    for alt in (220, 240, 260, 280, 700, 900, 920, 940, 1532, 1564, 1628, 1692):  # another form's int8 beams, same input and table: bitwise equal
         if alt not in tnames:
             continue
         outs = []
