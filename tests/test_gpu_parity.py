@@ -409,7 +409,10 @@ def fused_path(request):
     (64, 16, 4, 256, 3, 1, True), (64, 1, 4, 256, 2, 4, False), (4, 1, 64, 1024, 1, 64, False),
     (19, 2, 13, 256, 3, 1, False), (5, 3, 7, 48, 2, 7, True), (130, 9, 2, 64, 2, 1, False),
     (256, 64, 1, 32, 1, 1, True), (80, 2, 3, 16, 3, 3, False), (64, 16, 700, 256, 2, 1, False),
-    (32, 24, 9, 128, 5, 9, True)])
+    (32, 24, 9, 128, 5, 9, True),
+    # the wide kernel's 32-beam slabs with a pulled-back last k-step (A % 16 != 0), a partial last slab, a partial
+    # sample chunk and per-channel models: the phasor pairs' uniform/lane addressing at every edge it has
+    (200, 40, 3, 96, 2, 3, True), (72, 33, 2, 64, 1, 1, False)])
 @pytest.mark.parametrize("exact", [False, True])
 def test_fused_matches_oracle(context, command_queue, fused_path, exact, A, M, C, T, B, dch, signed):
     Ctot, xeng = 8192, 3
