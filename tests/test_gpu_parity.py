@@ -571,7 +571,9 @@ def test_errors_raise(context, command_queue):
 
 
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
-    (64, 16, 3, 256, 2, 1, True), (19, 3, 4, 48, 2, 4, False), (130, 9, 2, 64, 1, 1, True), (33, 8, 2, 64, 2, 2, False)])
+    (64, 16, 3, 256, 2, 1, True), (19, 3, 4, 48, 2, 4, False), (130, 9, 2, 64, 1, 1, True), (33, 8, 2, 64, 2, 2, False),
+    # the wide kernel's 32-beam slabs with weights: config 4's item shape, and a pulled-back step + partial slab
+    (256, 64, 1, 32, 1, 1, False), (200, 40, 2, 96, 1, 2, True)])
 @pytest.mark.parametrize("exact", [False, True])
 def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, T, B, dch, signed):
     """?beam-weights (corr3_servlet.py:140-153): per-(beam, input) weights folded into the phasors, set through the
