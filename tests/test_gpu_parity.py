@@ -606,7 +606,10 @@ def test_fused_beam_weights(context, command_queue, fused_path, exact, A, M, C, 
 
 @pytest.mark.parametrize("A,M,C,T,B,dch,signed", [
     (64, 16, 3, 256, 2, 1, True), (64, 16, 2, 256, 2, 1, False), (19, 3, 4, 48, 2, 4, False),
-    (130, 9, 2, 64, 1, 1, True)])
+    (130, 9, 2, 64, 1, 1, True),
+    # the 32-beam int8 kernels (Q14 table generator with gains / in-kernel phasors) at 256 antennas x 64 beams, and a
+    # pulled-back antenna step with a partial slab and per-channel models
+    (256, 64, 2, 64, 1, 1, True), (200, 40, 2, 96, 1, 2, True)])
 @pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel"])
 def test_fused_int8_beam_weights_bit_exact(context, command_queue, i8_kernel, A, M, C, T, B, dch, signed):
     """Weighted int8 beams: Q14 limbs of the weighted float32 coefficients, bit-exact to the integer contract."""
