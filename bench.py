@@ -188,7 +188,7 @@ def scatter_inputs(args, dist, shape):
         report["rccl_bytes_received_this_rank"] = received
         report["rccl_bytes_sent_root"] = sent if rank == 0 else None
         report["collective"] = ("RCCL grouped ncclSend/ncclRecv over xGMI via libbf bf_channel_scatter, device to "
-                                "device (root: one 2-D pack per rank, its own slice by a self send/recv)")
+                                "device (root: one 2-D pack per peer, its own slice by a 2-D copy -- at one rank by a self send/recv)")
     else:
         full = None
         if rank == 0:

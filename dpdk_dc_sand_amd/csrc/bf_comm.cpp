@@ -5,11 +5,14 @@
 // host thread per device (utilities/pcie_bandwidth_tests/main.cpp:193-224, cudaPcieRateTest.cpp:9).  Here one
 // process drives one GPU (rank r = X-engine r) and the root hands every rank its channel slice of a full-band
 // voltage cube once, device to device over xGMI:
-//   root: every rank's slice (B * A strided runs of C*T*4 bytes in the (B, A, C*N, T, 2, 2) band) is packed into a
-//         contiguous staging block by one 2-D copy, then one RCCL group: a ncclSend per rank -- each peer's bytes
-//         on their own xGMI link at once -- and the root's own ncclRecv of its slice (a self send/recv, so the
-//         same RCCL point-to-point path runs at one rank as at N: the one-GPU box exercises it);
-//   peers: one ncclRecv of the whole slice into the (B, A, C, T, 2, 2) input buffer of the fused beamformer.
+//   root: every peer's slice (B * A strided runs of C*T*4 bytes in the (B, A, C*N, T, 2, 2) band) is packed into a
+//         contiguous staging block by 2-D copies, then RCCL groups of one ncclSend per peer -- each peer's bytes on
+//         their own xGMI link at once; the root's own slice is a 2-D copy straight into `slice`.  At one rank the
+//         root's slice instead goes pack -> self ncclSend/ncclRecv, so the one-GPU box exercises the same RCCL
+//         point-to-point path the N-rank node runs;
+//   peers: ncclRecv of the slice into the (B, A, C, T, 2, 2) input buffer of the fused beamformer.
+// The slice moves in pieces of at most 256 MiB (whole rows, or segments of a row longer than that), one RCCL group
+// per piece.
 // Everything is ordered on the caller's stream; nothing on the beamforming hot path touches RCCL.  Every rank
 // records `done` after its part of each scatter; bf_comm_destroy waits for it before tearing the communicator down.
 // bf_checksum (position-weighted 64-bit sum of a 2-D byte region) lets the ranks verify what they received against
@@ -94,12 +97,46 @@ int rccl_fail(ncclResult_t e, const char* what) {
 
 }  // namespace
 
-constexpr size_t kScatterChunk = size_t(256) << 20;  // bytes per RCCL group of a scatter (whole rows)
+// Bytes per RCCL group of a scatter.  A piece is a block of whole (b, a) rows, or a segment of one row when a row is
+// longer than this: no group moves more.  On the one-GPU box a single 2 GiB self send/recv of a packed slice left the
+// second GiB unwritten (round 4, tools/diag_scatter.py); with these pieces every size verifies.
+constexpr size_t kScatterChunk = size_t(256) << 20;
+#ifdef BF_DIAG
+size_t g_scatter_chunk = kScatterChunk;  // measurement knob (bf_diag_scatter_chunk): attribute the truncation
+inline size_t scatter_chunk() { return g_scatter_chunk; }
+#else
+constexpr size_t scatter_chunk() { return kScatterChunk; }
+#endif
+
+namespace {
+// One piece of a slice: `nrows` rows from `row0`, bytes [off, off + width) of each.  Either width == run (whole rows,
+// contiguous in the packed slice) or nrows == 1 (a row segment): a piece is always one contiguous run of nrows * width
+// bytes of the packed slice, at row0 * run + off.
+struct Piece {
+  size_t row0, nrows, off, width;
+};
+
+// Calls f(piece) for every piece of a slice of `rows` runs of `run` bytes, in the same order on every rank (the
+// root's sends and each peer's receives pair up group by group); stops at the first non-zero status.
+template <class F>
+int for_each_piece(size_t rows, size_t run, size_t chunk, F&& f) {
+  if (run <= chunk) {
+    const size_t per = chunk / run;
+    for (size_t r0 = 0; r0 < rows; r0 += per)
+      if (const int st = f(Piece{r0, std::min(per, rows - r0), 0, run})) return st;
+  } else {
+    for (size_t r = 0; r < rows; ++r)
+      for (size_t off = 0; off < run; off += chunk)
+        if (const int st = f(Piece{r, 1, off, std::min(chunk, run - off)})) return st;
+  }
+  return BF_OK;
+}
+}  // namespace
 
 struct bf_comm {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0, device = 0;
-  void* staging = nullptr;  // root: (nranks - 1) packed peer slices
+  void* staging = nullptr;  // root: the packed peer slices (N - 1 of them; at one rank the root's own, for the self path)
   size_t staging_bytes = 0;
   double* d_scalar = nullptr;  // allreduce scratch
   hipStream_t stream = nullptr;
@@ -217,12 +254,14 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
   const size_t pitch = run * static_cast<size_t>(c->nranks);    // the band's (b, a) row
   const size_t rows = static_cast<size_t>(B) * A;
   const size_t slice_bytes = run * rows;
-  // The slice moves in blocks of whole (b, a) rows of at most kScatterChunk bytes, one RCCL group per block: on the
-  // one-GPU box a single 2 GiB self send/recv (or its 2-D pack) left the second GiB of the slice unwritten
-  // (tools/diag_scatter.py: every slice up to 1 GiB arrived intact, 2047 and 2048 MiB did not).
-  const size_t rows_per = std::max<size_t>(1, kScatterChunk / run);
+  const size_t chunk = scatter_chunk();
   if (c->rank == root) {
-    const size_t need = slice_bytes * static_cast<size_t>(c->nranks);
+    // At one rank the root's slice goes through RCCL too (pack, then a self ncclSend/ncclRecv), so the one-GPU box
+    // runs the point-to-point path of N ranks.  At N > 1 the root's own slice is one 2-D copy (no staging round
+    // trip: a deployment never needs it) and only the N - 1 peer slices are packed.
+    const bool self_p2p = c->nranks == 1;
+    const int npeers = self_p2p ? 1 : c->nranks - 1;
+    const size_t need = slice_bytes * static_cast<size_t>(npeers);
     if (need > c->staging_bytes) {
       if (c->staging) {
         BF_HIP(hipEventSynchronize(c->sent));
@@ -236,15 +275,21 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
     // the previous scatter's sends may still read the staging buffer on another stream
     BF_HIP(hipStreamWaitEvent(st, c->sent, 0));
     uint8_t* stg = static_cast<uint8_t*>(c->staging);
-    for (size_t r0 = 0; r0 < rows; r0 += rows_per) {
-      const size_t nr = std::min(rows_per, rows - r0), off = r0 * run, bytes = nr * run;
-      for (int r = 0; r < c->nranks; ++r)
-        BF_HIP(hipMemcpy2DAsync(stg + slice_bytes * static_cast<size_t>(r) + off, run,
-                                band + r0 * pitch + run * static_cast<size_t>(r), pitch, run, nr,
+    auto slot = [&](int r) {  // the peer's packed slice in staging
+      return stg + slice_bytes * static_cast<size_t>(self_p2p ? 0 : (r < root ? r : r - 1));
+    };
+    const int st_pieces = for_each_piece(rows, run, chunk, [&](const Piece& pc) -> int {
+      const size_t off = pc.row0 * run + pc.off, bytes = pc.nrows * pc.width;
+      const uint8_t* src = band + pc.row0 * pitch + pc.off;
+      for (int r = 0; r < c->nranks; ++r) {
+        uint8_t* dst = (r == root && !self_p2p) ? slice + off : slot(r) + off;
+        BF_HIP(hipMemcpy2DAsync(dst, run, src + run * static_cast<size_t>(r), pitch, pc.width, pc.nrows,
                                 hipMemcpyDeviceToDevice, st));
+      }
       BF_RCCL(rccl().group_start());
       for (int r = 0; r < c->nranks; ++r) {
-        ncclResult_t e = rccl().send(stg + slice_bytes * static_cast<size_t>(r) + off, bytes, ncclUint8, r, c->comm, st);
+        if (r == root && !self_p2p) continue;
+        ncclResult_t e = rccl().send(slot(r) + off, bytes, ncclUint8, r, c->comm, st);
         if (e == ncclSuccess && r == root) e = rccl().recv(slice + off, bytes, ncclUint8, root, c->comm, st);
         if (e != ncclSuccess) {
           (void)rccl().group_end();
@@ -252,16 +297,20 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
         }
       }
       BF_RCCL(rccl().group_end());
-    }
+      return BF_OK;
+    });
+    if (st_pieces != BF_OK) return st_pieces;
     BF_HIP(hipEventRecord(c->sent, st));
-    c->p2p_sent += slice_bytes * static_cast<unsigned long long>(c->nranks);
+    c->p2p_sent += slice_bytes * static_cast<unsigned long long>(npeers);
+    if (self_p2p) c->p2p_received += slice_bytes;
   } else {
-    for (size_t r0 = 0; r0 < rows; r0 += rows_per) {
-      const size_t nr = std::min(rows_per, rows - r0);
-      BF_RCCL(rccl().recv(slice + r0 * run, nr * run, ncclUint8, root, c->comm, st));
-    }
+    const int st_pieces = for_each_piece(rows, run, chunk, [&](const Piece& pc) -> int {
+      BF_RCCL(rccl().recv(slice + pc.row0 * run + pc.off, pc.nrows * pc.width, ncclUint8, root, c->comm, st));
+      return BF_OK;
+    });
+    if (st_pieces != BF_OK) return st_pieces;
+    c->p2p_received += slice_bytes;
   }
-  c->p2p_received += slice_bytes;
   BF_HIP(hipEventRecord(c->done, st));
   c->pending = true;
   bf::clear_error();
@@ -280,5 +329,35 @@ int bf_comm_load(void) {
   bf::clear_error();
   return BF_OK;
 }
+
+#ifdef BF_DIAG
+// ---- diagnostic build: attributing the round-4 2 GiB truncation (tools/diag_scatter.py --attribute) ----
+// The scatter's piece size; 0 restores the product's.
+int bf_diag_scatter_chunk(size_t bytes) {
+  g_scatter_chunk = bytes ? bytes : kScatterChunk;
+  return BF_OK;
+}
+// The pack stage alone: one hipMemcpy2DAsync of `height` rows of `width` bytes (pitches as given).
+int bf_diag_memcpy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
+                     void* stream) {
+  BF_HIP(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToDevice, bf::as_stream(stream)));
+  return BF_OK;
+}
+// The RCCL stage alone: one group of a self ncclSend(src) + ncclRecv(dst) of `bytes` on a one-rank communicator.
+int bf_diag_p2p_self(bf_comm* c, const void* src, void* dst, size_t bytes, void* stream) {
+  BF_REQUIRE(c != nullptr && c->nranks == 1, "bf_diag_p2p_self: needs a one-rank communicator");
+  DeviceGuard dg(c->device);
+  hipStream_t st = bf::as_stream(stream);
+  BF_RCCL(rccl().group_start());
+  ncclResult_t e = rccl().send(src, bytes, ncclUint8, 0, c->comm, st);
+  if (e == ncclSuccess) e = rccl().recv(dst, bytes, ncclUint8, 0, c->comm, st);
+  if (e != ncclSuccess) {
+    (void)rccl().group_end();
+    return rccl_fail(e, "bf_diag_p2p_self");
+  }
+  BF_RCCL(rccl().group_end());
+  return BF_OK;
+}
+#endif  // BF_DIAG
 
 }  // extern "C"

@@ -12,6 +12,7 @@ the timed hot path:
 No torch: every rank runs libbf on one HIP runtime.
 """
 import ctypes
+import json
 
 import numpy as np
 
@@ -92,8 +93,8 @@ class ChannelScatter:
 
     def scatter(self, band, out, B, A, C, T, queue, root=0):
         """Stream-ordered on `queue`: band (B, A, C*N, T, 2, 2) device array on `root` (None elsewhere) -> `out`
-        (B, A, C, T, 2, 2) device array on every rank, written only by RCCL (ncclRecv; the root's own slice by a self
-        send/recv)."""
+        (B, A, C, T, 2, 2) device array on every rank: the peers' slices through RCCL (ncclSend/ncclRecv), the
+        root's own by a 2-D copy -- at one rank by a self send/recv instead, so one GPU runs the RCCL path too."""
         _lib.call("bf_channel_scatter", self.handle, _lib.ptr(band), _lib.ptr(out), B, A, C, T, root, queue.handle)
 
     def stats(self):
@@ -104,20 +105,24 @@ class ChannelScatter:
 
     def verify(self, band, out, B, A, C, T, queue, root=0):
         """Check every rank's received slice against the root's band without moving either to the host: each rank
-        checksums its slice (bf_checksum), the root checksums each rank's strided region of the band, and the root
-        compares them.  Returns (ok on every rank, [per-rank dict] on the root else None)."""
-        mine = device_checksum(out, C * T * 4 * B * A, 0, 1, queue)
-        got = self.group.gather_json({"rank": self.rank, "checksum": mine})
-        report, ok = None, True
+        checksums its slice (bf_checksum), the root checksums each rank's strided region of the band, rank 0 (the
+        host group's hub) compares them and every rank learns the outcome.  Returns (ok on every rank, [per-rank
+        dict] on the root else None)."""
+        if not 0 <= root < self.world:
+            raise ValueError(f"root {root} of {self.world} ranks")
+        payload = {"rank": self.rank, "checksum": device_checksum(out, C * T * 4 * B * A, 0, 1, queue)}
         if self.rank == root:
             run = C * T * 4
-            report = []
-            for g in got:
-                want = device_checksum(_lib.ptr(band) + run * g["rank"], run, run * self.world, B * A, queue)
-                report.append({"rank": g["rank"], "checksum": f"{g['checksum']:016x}", "match": g["checksum"] == want})
-            ok = all(r["match"] for r in report)
-        ok = not self.group.allreduce_any(not ok)
-        return ok, report
+            payload["want"] = [device_checksum(_lib.ptr(band) + run * r, run, run * self.world, B * A, queue)
+                               for r in range(self.world)]
+        got = self.group.gather_json(payload)
+        report = None
+        if self.rank == 0:
+            want = next(g["want"] for g in got if g["rank"] == root)
+            report = [{"rank": g["rank"], "checksum": f"{g['checksum']:016x}", "match": g["checksum"] == want[g["rank"]]}
+                      for g in sorted(got, key=lambda g: g["rank"])]
+        report = json.loads(self.group.broadcast_bytes(json.dumps(report).encode() if self.rank == 0 else None))
+        return all(r["match"] for r in report), (report if self.rank == root else None)
 
     def allreduce_max(self, value):
         v = ctypes.c_double(float(value))

@@ -32,7 +32,8 @@ extern "C" {
 
 /* Thread-local message of the last failing call on this thread (replaces GPU_ERRCHK's stderr print). */
 const char* bf_last_error(void);
-/* ABI version: major * 100 + minor. */
+/* ABI version: major * 100 + minor.  300: ABI 3.0 -- 0x0500 (BF_FUSED_PATH_WIDE16, accepted by 2.0) is rejected as an
+ * unknown path, and bf_coeff_gen_time_study, bf_comm_stats, bf_comm_load and bf_checksum were added. */
 int bf_abi_version(void);
 
 /* ---- runtime helpers (device memory, streams, events) -------------------------------------------------
@@ -142,7 +143,7 @@ int bf_beamform(const uint8_t* x, const float* w, float* y, int B, int P, int C,
 #define BF_FUSED_PATH_GENERIC 0x0300 /* any A, any T: groups of 64 antennas */
 #define BF_FUSED_PATH_WIDE 0x0400    /* many antennas x beams: multi-wave beam slabs (config 4) */
 /* (0x0200 and 0x0600 named two measured-slower kernels of ABI 1.x, and 0x0500 (WIDE16) the 16-beam int8 wide kernel
- * of ABI 2.0, since removed from the product (0x0500: the 16-beam float slabs are what WIDE picks for M <= 16; the
+ * of ABI 2.0, removed from the product in ABI 3.0 (0x0500: the 16-beam float slabs are what WIDE picks for M <= 16; the
  * int8 kernel lives on in the diagnostic build): all three are rejected as unknown.) */
 #define BF_FUSED_ORDER_MASK 0x3000
 #define BF_FUSED_ORDER_CHANNEL 0x1000 /* plain channel-fastest workgroup order */
@@ -220,10 +221,11 @@ int bf_pipeline_stage_ms(bf_pipeline* p, long long ticket, float* h2d_ms, float*
  *   bf_comm_unique_id : rank 0 makes the communicator id (BF_COMM_ID_BYTES); the caller hands it to every rank
  *   bf_comm_create    : collective over all ranks, on the device current at the call
  *   bf_channel_scatter: band (B, A, C*N, T, 2, 2) 8-bit on `root` (ignored elsewhere) -> slice (B, A, C, T, 2, 2) on
- *                       every rank; stream-ordered on `stream` (root: per-rank 2-D pack into a staging buffer of N
- *                       slices, grown on demand, then one RCCL group of ncclSend per rank plus the root's own
- *                       ncclRecv -- a self send/recv, so one rank runs the same point-to-point path as N; peers: one
- *                       ncclRecv).  `slice` is written only by ncclRecv.
+ *                       every rank; stream-ordered on `stream`, in pieces of at most 256 MiB (whole (b, a) rows,
+ *                       or segments of a longer row), one RCCL group per piece.  Root: each peer's slice 2-D packed
+ *                       into a staging buffer of N - 1 slices (grown on demand) and sent with ncclSend, its own slice
+ *                       one 2-D copy; at one rank the root's slice is packed and moved by a self ncclSend/ncclRecv
+ *                       instead, so one rank runs the point-to-point path of N.  Peers: ncclRecv per piece.
  *   bf_comm_allreduce_max: host value -> max over ranks (blocking; timing brackets and agreement checks)
  *   bf_comm_stats     : bytes this rank has handed to ncclSend / ncclRecv so far (the scatter's RCCL traffic)
  *   bf_comm_load      : BF_OK when RCCL can be loaded (a local precondition each rank checks before the collective

@@ -42,7 +42,7 @@ def test_prototypes_match_header():
 
 def test_abi_version_and_error_channel():
     lib = _lib.load()
-    assert lib.bf_abi_version() == 200
+    assert lib.bf_abi_version() == 300  # 3.0: WIDE16 (0x500) rejected, four entry points added
     assert isinstance(_lib.last_error(), str)
 
 
@@ -107,7 +107,7 @@ def test_pipeline_argument_validation_without_gpu():
 def test_kernel_path_and_contract_flags_are_validated():
     fake = 1 << 20
     args = [fake, fake, 1, fake, 1, 4, 16, 4, 1, 1024, 0, 1e-9, 0.0, 0.0]
-    for retired in (0x200, 0x500, 0x600, 0x700):  # removed measured-slower kernels (0x500: WIDE16, ABI 2.0)
+    for retired in (0x200, 0x500, 0x600, 0x700):  # removed measured-slower kernels (0x500: WIDE16, accepted by ABI 2.0, rejected since 3.0)
         with pytest.raises(_lib.BeamformerError, match="unknown kernel path"):
             _lib.call("bf_beamform_fused", *args, retired, 1.0, None)
     with pytest.raises(_lib.BeamformerError, match="unknown workgroup order"):

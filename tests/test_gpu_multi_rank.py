@@ -145,15 +145,17 @@ def test_bench_rccl_scatter_path_one_rank(tmp_path):
     assert line["value"] > 0
 
 
-def _visible_devices():
-    import torch  # device_count() does not initialise the GPU on this image
-    return torch.cuda.device_count()
-
-
-@pytest.mark.skipif(_visible_devices() < 2, reason="the RCCL channel scatter across ranks needs two GPUs")
 def test_bench_rccl_scatter_two_ranks(tmp_path):
     """bench.py --gpus 2 over RCCL (one rank per GPU): the root's band is packed and sent to both ranks, and every
-    rank's received slice is checksummed on its device and compared with the root's band slice [C r, C (r + 1))."""
+    rank's received slice is checksummed on its device and compared with the root's band slice [C r, C (r + 1)).
+
+    The device count comes from libbf (the product's /opt/rocm HIP runtime) inside the test: a collection-time
+    `torch.cuda.device_count()` would map torch's bundled HIP runtime into the test process first, and every later
+    libbf load would then bind to it (test_hip_runtime_is_the_products)."""
+    sys.path.insert(0, ROOT)
+    from dpdk_dc_sand_amd import accel
+    if accel.device_count() < 2:
+        pytest.skip("the RCCL channel scatter across ranks needs two GPUs")
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",

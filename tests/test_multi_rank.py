@@ -207,3 +207,58 @@ def test_checksum_and_comm_stats_argument_validation_without_gpu():
     _lib.call("bf_checksum", 1 << 20, 0, 0, 3, ctypes.byref(out), None)  # empty region: 0, no device touched
     with pytest.raises(_lib.BeamformerError, match="null pointer"):
         _lib.call("bf_comm_stats", None, ctypes.byref(out), ctypes.byref(out))
+
+
+class _FakeDev:
+    """A host array standing in for a device buffer: `ptr` is a fake address resolved by _fake_checksum."""
+    registry = {}
+
+    def __init__(self, arr, base):
+        self.arr, self.ptr = np.ascontiguousarray(arr).reshape(-1).view(np.uint8), base
+        _FakeDev.registry[base] = self
+
+
+def _fake_checksum(src, run_bytes, pitch_bytes, rows, queue):
+    from dpdk_dc_sand_amd.shard import host_checksum
+    addr = src.ptr if isinstance(src, _FakeDev) else int(src)
+    base = max(b for b in _FakeDev.registry if b <= addr)
+    buf = _FakeDev.registry[base].arr[addr - base:]
+    pitch = pitch_bytes or run_bytes
+    return host_checksum(np.concatenate([buf[i * pitch:i * pitch + run_bytes] for i in range(rows)]))
+
+
+def _verify_worker(rank, world, port, q, root, bad_rank):
+    """ChannelScatter.verify over a world-`world` host group with the device checksums replaced by the host
+    restatement: every rank's slice is compared with the root's band region, whichever rank is the root."""
+    from dpdk_dc_sand_amd import shard
+    from dpdk_dc_sand_amd.rendezvous import HostGroup
+    try:
+        shard.device_checksum = _fake_checksum
+        g = HostGroup(rank, world, "127.0.0.1", port)
+        B, A, C, T = 2, 3, 4, 8
+        band = np.random.default_rng(1).integers(0, 256, (B, A, C * world, T, 2, 2), dtype=np.uint8)
+        mine = pack_channel_slices(band, world)[rank].copy()
+        if rank == bad_rank:
+            mine[1, 2, 3, 4, 1, 0] ^= 1
+        cs = shard.ChannelScatter.__new__(shard.ChannelScatter)
+        cs.group, cs.rank, cs.world, cs.handle = g, rank, world, None
+        ok, report = cs.verify(_FakeDev(band, 1 << 40) if rank == root else None, _FakeDev(mine, 1 << 41), B, A, C,
+                               T, None, root=root)
+        g.close()
+        q.put((rank, "ok", ok, report))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, "error " + repr(e), None, None))
+
+
+@pytest.mark.parametrize("root,bad_rank", [(0, None), (1, None), (2, 0), (1, 2)])
+def test_scatter_verify_any_root(root, bad_rank):
+    world = 3
+    res = _run_world(_verify_worker, world, root, bad_rank)
+    assert all(r[1] == "ok" for r in res), res
+    assert all(r[2] == (bad_rank is None) for r in res), res
+    for rank, _, _, report in res:
+        if rank != root:
+            assert report is None
+        else:
+            assert [x["rank"] for x in report] == [0, 1, 2]
+            assert [x["match"] for x in report] == [r != bad_rank for r in range(world)]
