@@ -98,8 +98,11 @@ int rccl_fail(ncclResult_t e, const char* what) {
 }  // namespace
 
 // Bytes per RCCL group of a scatter.  A piece is a block of whole (b, a) rows, or a segment of one row when a row is
-// longer than this: no group moves more.  On the one-GPU box a single 2 GiB self send/recv of a packed slice left the
-// second GiB unwritten (round 4, tools/diag_scatter.py); with these pieces every size verifies.
+// longer than this: no group moves more.  Why: RCCL 2.27.7's point-to-point drops bytes of large messages -- a
+// single self ncclSend/ncclRecv of more than 1 GiB leaves every byte past 2^30 unwritten, while the 2-D pack of the
+// same slice (hipMemcpy2DAsync) is intact; attributed stage by stage on the device (tools/diag_scatter.py
+// --attribute, profiles/r5_a_scatter_attribution.txt: 1 GiB ok; 2047 and 2048 MiB wrong from byte 2^30 on, pack ok).
+// With 256 MiB pieces every size verifies (tests/test_gpu_multi_rank.py: 2 GiB slices, rows over 256 MiB).
 constexpr size_t kScatterChunk = size_t(256) << 20;
 #ifdef BF_DIAG
 size_t g_scatter_chunk = kScatterChunk;  // measurement knob (bf_diag_scatter_chunk): attribute the truncation

@@ -423,6 +423,20 @@ __device__ __forceinline__ void w32_load(const uint8_t* __restrict__ base, size_
 template <int Mode>
 __device__ __forceinline__ void w32_load_buf(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t sbase, uint32_t stride,
                                              u32x2_t (&d)[8]) {
+  if constexpr ((Mode & 256) != 0) {
+    // diagnostics (timing only, wrong beams): the same bytes in half the instructions -- lane pair (tl, tl ^ 1) loads
+    // 16 bytes of row 2q + (tl & 1) at the pair's sample offset, without the swap that would hand each lane its own
+    // rows back: is the TA's address rate (8-byte lane loads) what bounds the kernel?
+    const uint32_t odd = (voff >> 3) & 1;  // tl & 1 (voff = hoff + 8 tl)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const u32x4_t v = __builtin_bit_cast(
+          u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff - 8 * odd + odd * stride, sbase + 2 * q * stride, 0));
+      d[2 * q] = u32x2_t{v[0], v[1]};
+      d[2 * q + 1] = u32x2_t{v[2], v[3]};
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     if constexpr (Mode & 8) {
@@ -1111,6 +1125,288 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
   }
 }
 
+// ---- config 4's shape: a wave-private LDS-DMA voltage ring over the halved limb image (round 5) --------------------
+// The table kernel above loads each wave-step's 4 KiB of voltages as 8 buffer_load_dwordx2 per lane (512 B per
+// instruction): per CU and channel 1024 such instructions (both slabs) -- as many TA address cycles as the channel's
+// MFMA cycles (SQ_VMEM_TA_ADDR_FIFO_FULL 1.06e8 per launch, r4_t).  Here a wave DMAs its step into LDS with four
+// 1 KiB `buffer_load_dwordx4 ... lds` (half the TA cycles, no VGPR destination) and reads it back with eight
+// ds_read_b64 in exactly the register layout of the table kernel.  The LDS for that comes from the halved image
+// (y_re = [x_re, x_im].(Wc, -Ws), y_im = [x_im, ~x_re].(Wc, -Ws) + sum_a Ws -- same MFMAs, half the A fragments):
+// 32 KiB of image + 2 x 16 KiB of slots + 512 B of column sums per workgroup, two workgroups per CU.
+//   ring: step n's voltages in slot n & 1 of the wave (DMA'd two steps ahead); each step reads its slot, builds its
+//         fragments, then DMAs step n + 2 into the same slot (the compiler counts the DMA in vmcnt and waits for it
+//         before the slot's next read only: the slots are distinct __shared__ objects);
+//   image: expanded from the kLayoutW32 table (the q14_table_kernel generator) into (Wc, -Ws) limb pairs after each
+//         channel barrier, the slab's sum_a Ws per beam reduced through LDS (y_im's bias);
+//   slot layout: antenna row 8h + q of the step at position 4q + h (128 B each), so the two lane halves of a
+//         ds_read_b64 read adjacent 128 B rows (no bank conflict); the DMA writes lane-linearly, so the permutation
+//         goes on its source address (lane i of instruction k: antenna 8((i >> 3) & 3) + 2k + (i >> 5), bytes
+//         16 (i & 7) of the wave's 128-byte sample run).
+// Shape: int8 voltages, 8 k-steps (224 < A <= 256), T = 256 (2 passes of 8 straight-line steps), M % 32 == 0,
+// in-workgroup voltage offsets and the beams below 2^31 bytes; 8 channels per workgroup.
+constexpr int kW32RChannels = 8;
+__shared__ __attribute__((aligned(16))) int4 w32r_img[8 * 2 * 2 * 64];  // [step][tile][limb][lane] x 16 B
+__shared__ __attribute__((aligned(16))) int4 w32r_slot0[4 * 256];       // [wave][4 KiB]: even steps
+__shared__ __attribute__((aligned(16))) int4 w32r_slot1[4 * 256];       // odd steps
+__shared__ __attribute__((aligned(16))) int w32r_ws[4 * 32];            // [wave][beam] partial sum_a Ws
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// One table unit (beam ml, slot-antenna group g: step g >> 2, lane group g & 3) -> the halved image's two entries:
+// per antenna the (Wc, -Ws) pair as balanced limbs (lo = byte 0 as int8, hi = byte 1 of W + 128), w32_expand_unit's
+// column-2 ml entries at the halved layout's place.
+__device__ __forceinline__ void w32r_expand_unit(int4* img, int ml, int g, const u32x4_t& q0, const u32x4_t& q1) {
+  const uint32_t d[8] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
+  uint32_t n[8], np[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const u16x2_t neg = __builtin_bit_cast(u16x2_t, d[i]) * u16x2_t{1, 0xffff};  // (Wc, -Ws)
+    n[i] = __builtin_bit_cast(uint32_t, neg);
+    np[i] = __builtin_bit_cast(uint32_t, neg + u16x2_t{128, 128});
+  }
+  u32x4_t ehi, elo;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    elo[q] = __builtin_amdgcn_perm(n[2 * q + 1], n[2 * q], 0x06040200u);
+    ehi[q] = __builtin_amdgcn_perm(np[2 * q + 1], np[2 * q], 0x07050301u);
+  }
+  int4* o = img + ((g >> 2) * 2 + (ml >> 4)) * 2 * 64 + (ml & 15) + 16 * (g & 3);
+  o[0] = __builtin_bit_cast(int4, ehi);
+  o[64] = __builtin_bit_cast(int4, elo);
+}
+
+// y_im's B fragment from y_re's: [x_re, x_im, ...] -> [x_im, ~x_re, ...] per antenna (~x = -x - 1 stays in int8).
+__device__ __forceinline__ i32x4_t w32r_frag_im(const i32x4_t& f) {
+  i32x4_t r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t n = static_cast<uint32_t>(f[q]) ^ 0x00ff00ffu;
+    r[q] = static_cast<int>(__builtin_amdgcn_perm(n, n, 0x02030001u));
+  }
+  return r;
+}
+
+// Mode (diagnostics only): 4 no stores, 8 no voltage DMA (the slots' stale bytes), 16 no table loads / expansion.
+template <bool Pow2, int Mode = 0>
+__global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(FusedArgs P) {
+  constexpr int Sp = 8, NP = 2, kCh = kW32RChannels;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 4, tl = lane & 15;
+  const int C = P.C;
+  const int gpb = (C + kCh - 1) / kCh;  // channel groups per batch
+  int slab, grp;
+  if (P.xcd_order) {  // the slabs of one channel group back to back on one XCD: the second re-reads from L2
+    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
+    slab = local % P.nslabs;
+    grp = (local / P.nslabs) * 8 + x;
+    if (grp >= P.B * gpb) return;
+  } else {
+    slab = blockIdx.x % P.nslabs;
+    grp = blockIdx.x / P.nslabs;
+  }
+  const int b = grp / gpb, c0 = (grp - b * gpb) * kCh;
+  const int nk = min(kCh, C - c0);
+  const int m0 = slab * kW32Beams;
+  const uint32_t ant_stride = static_cast<uint32_t>(C) * static_cast<uint32_t>(P.T) * 4u;  // host: A C T 4 < 2^31
+  const uint32_t ch_bytes = static_cast<uint32_t>(P.T) * 4u;
+  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * C + c0) * static_cast<size_t>(P.T) * 4;
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7fffffff,
+                                                                        0x00020000);
+  const uint32_t dma_voff = static_cast<uint32_t>(8 * ((lane >> 3) & 3) + (lane >> 5)) * ant_stride +
+                            16u * static_cast<uint32_t>(lane & 7);
+  int4* const slot0 = w32r_slot0 + 256 * wave;
+  int4* const slot1 = w32r_slot1 + 256 * wave;
+
+  // the voltage ring: step ls of pass lp of channel lk is DMA'd next (past the last step it repeats that step)
+  const int total = nk * NP * Sp;
+  int issued = 0, ls = 0, lp = 0, lk = 0;
+  auto dma = [&](int4* slot) {
+    // (readfirstlane: a loop-carried part of it landed in a VGPR, and the DMA's soffset then became a waterfall loop)
+    const uint32_t sb = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(w8_step_base(ls, P.A)) * ant_stride + static_cast<uint32_t>(lk) * ch_bytes +
+        static_cast<uint32_t>(wave + 4 * lp) * 128u);
+    if constexpr ((Mode & 8) == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lds_void_ptr)(slot + 64 * k), 16, dma_voff,
+                                                 sb + 2u * static_cast<uint32_t>(k) * ant_stride, 0, 0);
+    }
+    ++issued;
+    const bool adv = issued < total;
+    const bool wrap = ls + 1 == Sp, pwrap = lp + 1 == NP;
+    ls = adv ? (wrap ? 0 : ls + 1) : ls;
+    lp = (adv && wrap) ? (pwrap ? 0 : lp + 1) : lp;
+    lk = (adv && wrap && pwrap) ? lk + 1 : lk;
+  };
+  // this lane's 8 antenna rows x its sample pair from the wave's slot: the table kernel's register layout
+  auto read_slot = [&](const int4* slot, u32x2_t (&d)[8]) {
+    const u32x2_t* s2 = reinterpret_cast<const u32x2_t*>(slot);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d[q] = s2[(4 * q + h) * 16 + tl];
+  };
+
+  // the channel's table units (kLayoutW32: two 16-byte loads per unit, a buffer resource on the channel's block)
+  const u32x4_t* tbase = reinterpret_cast<const u32x4_t*>(P.table) +
+                         ((static_cast<size_t>(b) * C + c0) * P.nslabs + slab) * 256 * Sp;
+  const size_t tstride = static_cast<size_t>(P.nslabs) * 256 * Sp;  // u32x4 per channel
+  u32x4_t tq[4][2];
+  auto load_table = [&](int kc) {
+    if constexpr ((Mode & 16) == 0) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<u32x4_t*>(tbase + static_cast<size_t>(kc) * tstride), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+          tq[j][hf] = __builtin_bit_cast(
+              u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<uint32_t>(((j * 2 + hf) * 256 + tid) * 16), 0, 0));
+    }
+  };
+  // the image of the staged channel + this wave's partial sum_a Ws per beam (lanes ml and ml + 32 hold the same beam)
+  auto expand = [&]() {
+    if constexpr ((Mode & 16) == 0) {
+      const int ml = tid & 31;
+      int ws = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w32r_expand_unit(w32r_img, ml, (tid >> 5) + 8 * j, tq[j][0], tq[j][1]);
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ws += static_cast<int>(tq[j][hf][q]) >> 16;
+      }
+      ws += __shfl_xor(ws, 32);
+      if (lane < 32) w32r_ws[32 * wave + ml] = ws;
+    }
+  };
+
+  load_table(0);
+  __builtin_amdgcn_sched_barrier(0);
+  dma(slot0);
+  dma(slot1);
+  __builtin_amdgcn_sched_barrier(0);
+  expand();
+  lds_barrier();
+
+  const float s32 = P.out_scale * 0x1p-14f;
+  const int M2 = 2 * P.M;
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(P.y, 0, 0x7fffffff, 0x00020000);
+  // the lane's part of a beam-row store offset (sample 2 tl + i of the wave's 32, row piece of lane group h)
+  const uint32_t so_lane = static_cast<uint32_t>(2 * tl * M2 + 16 * (h >> 1) + 32 * (h & 1));
+  for (int kc = 0; kc < nk; ++kc) {
+    const int c = c0 + kc;
+#pragma unroll
+    for (int pass = 0; pass < NP; ++pass) {
+      i32x4_t rh[2][2][2], rl[2][2][2], ih[2][2][2], il[2][2][2];  // [pol][sample i][tile]
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) rh[p][i][t] = rl[p][i][t] = ih[p][i][t] = il[p][i][t] = i32x4_t{0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < Sp; ++s) {
+        int4* const slot = (s & 1) ? slot1 : slot0;  // (16 steps per channel: the parity is the step's)
+        u32x2_t d[8];
+        read_slot(slot, d);
+        i32x4_t f[2][2], fi[2][2];
+        w32_frags<true>(d, f);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) fi[p][i] = w32r_frag_im(f[p][i]);
+        __builtin_amdgcn_sched_barrier(0);  // the slot is read (fragments built) before it is refilled
+        dma(slot);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int4 x0 = w32r_img[((s * 2 + t) * 2 + 0) * 64 + lane];
+          const int4 x1 = w32r_img[((s * 2 + t) * 2 + 1) * 64 + lane];
+          const i32x4_t ahi = i32x4_t{x0.x, x0.y, x0.z, x0.w}, alo = i32x4_t{x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              rh[p][i][t] = mfma_i8(ahi, f[p][i], rh[p][i][t]);
+              rl[p][i][t] = mfma_i8(alo, f[p][i], rl[p][i][t]);
+              ih[p][i][t] = mfma_i8(ahi, fi[p][i], ih[p][i][t]);
+              il[p][i][t] = mfma_i8(alo, fi[p][i], il[p][i][t]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // the next channel's table, requested after the last pass's MFMAs (its latency under the stores and barrier)
+      if (pass == NP - 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        load_table(min(kc + 1, nk - 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // requantise + store: lane (tl, h) holds beams 16 t + 4 h + r (re and im) of samples 2 tq2 + i; per tile two
+      // dwords [re, im, re, im] = bytes [32 t + 8 h, + 8) of the slab's 64-byte row; one permlane16_swap per dword
+      // pair gives lane group h the 16 bytes at 16 (h >> 1) + 32 (h & 1).
+      int bias[2][4];  // -sum_a Ws of beams 16 t + 4 h + r (y_im's bias)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        int4 acc = int4{0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int4 v = *reinterpret_cast<const int4*>(w32r_ws + 32 * w + 16 * t + 4 * h);
+          acc.x += v.x;
+          acc.y += v.y;
+          acc.z += v.z;
+          acc.w += v.w;
+        }
+        bias[t][0] = -acc.x;
+        bias[t][1] = -acc.y;
+        bias[t][2] = -acc.z;
+        bias[t][3] = -acc.w;
+      }
+      if constexpr ((Mode & 4) != 0) {
+        int sum = 0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) sum += rh[p][i][t][0] ^ rl[p][i][t][1] ^ ih[p][i][t][2] ^ il[p][i][t][3] ^ bias[t][p];
+        if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[tid] = sum;
+      } else {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const uint32_t prow = static_cast<uint32_t>(((b * 2 + p) * C + c) * P.T);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            uint32_t pk[2][2];  // [tile][dword]
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              uint32_t qr[4], qi[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                qr[r] = requant_bits<Pow2>((rh[p][i][t][r] << 8) + rl[p][i][t][r], s32);
+                qi[r] = requant_bits<Pow2>((ih[p][i][t][r] << 8) + il[p][i][t][r] + bias[t][r], s32);
+              }
+              pk[t][0] = pack_low_bytes(qr[0], qi[0], qr[1], qi[1]);
+              pk[t][1] = pack_low_bytes(qr[2], qi[2], qr[3], qi[3]);
+            }
+            const auto sw0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+            const auto sw1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(u32x4_t, u32x4_t{sw0[0], sw1[0], sw0[1], sw1[1]}), yrs, so_lane,
+                (prow + static_cast<uint32_t>(2 * (wave + 4 * pass) * 16 + i)) * static_cast<uint32_t>(M2) +
+                    static_cast<uint32_t>(2 * m0),
+                0);
+          }
+        }
+      }
+    }
+    if (kc + 1 < nk) {
+      lds_barrier();  // every wave is done with this channel's image and column sums
+      expand();
+      lds_barrier();
+    }
+  }
+}
+
 // ---- the halved-image contraction at config 4's shape (the default with a workspace there) ----------------------
 // The table (q14_image_kernel, kLayoutW32H) is the LDS image itself: per (b, c, slab) the (Wc, -Ws) limb fragments of
 // 32 beams x 8 k-steps (32 KiB, half the w32t kernel's image) and the slab's column sums.  A workgroup copies the
@@ -1614,6 +1910,29 @@ int launch_w64h_contract(FusedArgs P, hipStream_t st) {
   BF_LAUNCHED("beamform_fused_i8_w64h_kernel");
 }
 
+// The LDS-DMA ring contraction's shape (beamform_fused_i8_w32r_kernel): 8 k-steps, T = 256, whole 32-beam slabs,
+// every in-workgroup voltage offset and every beam offset below 2^31, a whole launch (no channel chunk).
+bool w32r_fits(const FusedArgs& P) {
+  return w32_steps(P.A) == 8 && P.A > 224 && P.T == 256 && P.M % kW32Beams == 0 && P.c_count == 0 &&
+         static_cast<unsigned long long>(P.A) * P.C * P.T * 4 < (1ull << 31) &&
+         static_cast<unsigned long long>(P.B) * 2 * P.C * P.T * 2 * P.M < (1ull << 31);
+}
+
+// The LDS-DMA ring contraction of one launch whose kLayoutW32 table is ready in P.table on `st` (int8 voltages).
+template <int Mode = 0>
+int launch_w32r_contract(FusedArgs P, hipStream_t st) {
+  const long long groups = static_cast<long long>(P.B) * ((P.C + kW32RChannels - 1) / kW32RChannels);
+  const long long grid = P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs;
+  BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
+  if (scale_is_pow2(P.out_scale * 0x1p-14f))
+    hipLaunchKernelGGL((beamform_fused_i8_w32r_kernel<true, Mode>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW8Threads), 0, st, P);
+  else
+    hipLaunchKernelGGL((beamform_fused_i8_w32r_kernel<false, Mode>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kW8Threads), 0, st, P);
+  BF_LAUNCHED("beamform_fused_i8_w32r_kernel");
+}
+
 // The halved-image contraction of one launch whose kLayoutW32H table is ready in P.table on `st`.
 template <bool Signed, int Mode = 0>
 int launch_w32h_contract(FusedArgs P, hipStream_t st) {
@@ -1678,6 +1997,8 @@ int launch_w32(FusedArgs P, hipStream_t st) {
 #endif
     const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32, st);
     if (e != BF_OK) return e;
+    if constexpr (Signed && Mode == 0)
+      if (w32r_fits(P)) return launch_w32r_contract(P, st);  // config 4's shape: the LDS-DMA voltage ring
     return launch_w32t_contract<Signed, Mode>(P, st);
   }
   if (P.gain)
@@ -1847,6 +2168,17 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
       default: return BF_ERR_ARG;
     }
   }
+  if (mode >= 2000 && mode < 2100) {  // the LDS-DMA ring contraction alone (the kLayoutW32 table); +Mode bits
+    switch (mode - 2000) {
+      case 0: return bf::launch_w32r_contract<0>(P, st);
+      case 4: return bf::launch_w32r_contract<4>(P, st);
+      case 8: return bf::launch_w32r_contract<8>(P, st);
+      case 12: return bf::launch_w32r_contract<12>(P, st);
+      case 16: return bf::launch_w32r_contract<16>(P, st);
+      case 24: return bf::launch_w32r_contract<24>(P, st);
+      default: return BF_ERR_ARG;
+    }
+  }
   if (mode >= 960 && mode < 1200) {  // the halved-image contraction alone (a kLayoutW32H table in `table`); +Mode bits
     P.nslabs = (M + 31) / 32;
     P.xcd_order = P.nslabs > 1;
@@ -1884,6 +2216,7 @@ extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, 
 #define BF_W32TP(m) \
   case 1500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8, true, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break
     BF_W32TP(32); BF_W32TP(33); BF_W32TP(36); BF_W32TP(40); BF_W32TP(64); BF_W32TP(128); BF_W32TP(192);
+    BF_W32TP(256); BF_W32TP(257); BF_W32TP(260);
 #undef BF_W32TP
     default: return BF_ERR_ARG;
   }

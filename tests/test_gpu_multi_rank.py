@@ -233,3 +233,31 @@ def test_device_checksum_matches_restatement():
     big = accel.DeviceArray(ctx, (1 << 26,), np.uint8)  # 64 MiB: many workgroups, one atomic per wave
     _lib.call("bf_fill_random", big.ptr, big.nbytes, 3, q.handle)
     assert device_checksum(big, big.nbytes, 0, 1, q) == host_checksum(big.get(q))
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 4096, 256), (1, 2, 294912, 256)], ids=["2GiB-slice", "rows-over-256MiB"])
+def test_channel_scatter_large_slices(shape):
+    """bf_channel_scatter at one rank with slices RCCL's point-to-point cannot move in one message: a 2 GiB slice
+    (RCCL 2.27.7's self ncclSend/ncclRecv of more than 1 GiB leaves every byte past 2^30 unwritten,
+    profiles/r5_a_scatter_attribution.txt) and rows longer than the 256 MiB piece (sub-row segments).  The device
+    checksums of every received slice must equal the band's."""
+    sys.path.insert(0, ROOT)
+    from dpdk_dc_sand_amd import _lib, accel
+    from dpdk_dc_sand_amd.rendezvous import HostGroup
+    from dpdk_dc_sand_amd.shard import ChannelScatter
+
+    B, A, C, T = shape
+    ctx = accel.create_some_context(device=0)
+    q = ctx.create_command_queue()
+    comm = ChannelScatter(HostGroup(0, 1), ctx)
+    try:
+        band = accel.DeviceArray(ctx, (B, A, C, T, 2, 2), np.uint8)
+        _lib.call("bf_fill_random", band.ptr, band.nbytes, 13, q.handle)
+        out = accel.DeviceArray(ctx, (B, A, C, T, 2, 2), np.uint8)
+        _lib.call("bf_fill_random", out.ptr, out.nbytes, 17, q.handle)
+        comm.scatter(band, out, B, A, C, T, q)
+        ok, report = comm.verify(band, out, B, A, C, T, q)
+        assert ok and report[0]["match"], report
+        assert comm.stats() == (band.nbytes, band.nbytes)
+    finally:
+        comm.close()

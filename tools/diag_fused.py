@@ -114,6 +114,10 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
                    if m in (0, 1, 4, 8)})
     tnames.update({1564: "full [NB2, 8 ch, buffer loads, nt table loads]", 1628: "full [NB2, 8 ch, buffer loads, nt voltage loads]",
                    1692: "full [NB2, 8 ch, buffer loads, nt table + voltage loads]"})
+    # round 5: the LDS-DMA voltage ring over the halved image (beamform_fused_i8_w32r_kernel) + its Mode bits
+    tnames.update({2000: "full [w32r: DMA ring, halved image]", 2004: "no-store [w32r]", 2008: "no voltage DMA [w32r]",
+                   2012: "no-store,no voltage DMA [w32r]", 2016: "no table [w32r]", 2024: "no table,no voltage DMA [w32r]"})
+    tnames.update({1756: "TA test: 16-B loads, wrong beams (spills)"})
     # 700 + m: the output-stationary LDS-DMA kernel (bf_wide_i8os.hip) on the same table; m = its Mode bits
     tnames.update({700 + m: v.replace("early ", "") + " [os, LDS-DMA]" for m, v in base.items() if m in (0, 1, 4, 8, 9, 12)})
     tnames.update({702: "no-mfma [os]", 705: "no table,no-store [os]",
@@ -135,7 +139,7 @@ if "w32t" in _os.environ.get("DIAG_KERNELS", ""):  # the table-driven 32-beam in
         if mode >= 0 and w32t_call(mode, 0) != 0:
             print(f"  w32t mode {mode}: launch failed: {lib.bf_last_error().decode(errors='replace')}")
             tnames.pop(mode)
-    for alt in (220, 240, 260, 280, 700, 900, 920, 940, 1532, 1564, 1628, 1692):  # another form's int8 beams, same input and table: bitwise equal
+    for alt in (220, 240, 260, 280, 700, 900, 920, 940, 1532, 1564, 1628, 1692, 2000):  # another form's int8 beams, same input and table: bitwise equal
         if alt not in tnames:
             continue
         outs = []

@@ -1,0 +1,15 @@
+#!/bin/bash
+# GPU box, round 5: the LDS-DMA ring contraction (w32r) -- parity on the config-4 tests, then the same-process A/B
+# against the table kernel (w32t) on one kLayoutW32 table.  Usage: bash tools/gpu_r5_w32r.sh <tag>
+set -o pipefail
+TAG=${1:-r5_w}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_fullsize.py tests/test_gpu_q14table.py -m gpu -x -v --timeout 120 \
+  --timeout-method thread -p no:cacheprovider > $OUT/pytest_cfg4.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_cfg4.log; exit 1; }
+tail -2 $OUT/pytest_cfg4.log
+DIAG_KERNELS=w32t W32T_MODES=${MODES:-900,2000,2004,2008,2012,2016,2024,908,901,904} DIAG_ROUNDS=5 timeout -k 10 300 \
+  python -u tools/diag_fused.py 1 4096 256 256 64 > $OUT/w32r_ab.txt 2>&1 || { echo "diag failed"; tail -20 $OUT/w32r_ab.txt; exit 1; }
+cat $OUT/w32r_ab.txt
+echo "run $TAG ok"
