@@ -1316,7 +1316,10 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
         for (int p = 0; p < 2; ++p)
 #pragma unroll
           for (int i = 0; i < 2; ++i) fi[p][i] = w32r_frag_im(f[p][i]);
-        __builtin_amdgcn_sched_barrier(0);  // the slot is read (fragments built) before it is refilled
+        // the slot's reads have returned (its bytes are in the fragments) before the DMA that refills it is issued:
+        // nothing else orders a ds_read before a later LDS-DMA write to the same bytes (WAR)
+        asm volatile("" ::"v"(f[0][0]), "v"(f[0][1]), "v"(f[1][0]), "v"(f[1][1]) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
         dma(slot);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -1405,6 +1408,9 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
       lds_barrier();
     }
   }
+  // The ring's last two DMAs (the last step again, unread) must land before the wave ends: an LDS-DMA still in
+  // flight when the workgroup's LDS is handed to the next workgroup on this CU would write into that workgroup's slots.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---- the halved-image contraction at config 4's shape (the default with a workspace there) ----------------------
