@@ -552,6 +552,22 @@ def mfma_util(wl, out_int8, int8_contract, kernel_s):
             "issued": round(issued / kernel_s / 1e12, 1), "frac_issued": round(issued / kernel_s / 1e12 / peak, 4)}
 
 
+def mfma_split(sec, ent):
+    """A two-kernel step (config 4's int8 path: the Q14 generator, then the contraction): the matrix-core rates of the
+    contraction alone, over its own rocprof time, and the generator's share of the step."""
+    per = ent.get("kernels_us_per_step")
+    if not per or "mfma" not in sec or "avg_us" not in ent:
+        return
+    contraction_us = ent["avg_us"]
+    total_us = ent.get("per_step_us_all_kernels") or sum(per.values())
+    scale = sec["avg_launch_us"] / contraction_us  # the rates scale with 1 / time
+    m = sec["mfma"]
+    m["contraction_only"] = {"kernel_us": contraction_us, "algorithmic": round(m["algorithmic"] * scale, 1),
+                             "issued": round(m["issued"] * scale, 1),
+                             "frac_issued": round(m["frac_issued"] * scale, 4)}
+    m["generator_share_of_step"] = round(1.0 - contraction_us / total_us, 4)
+
+
 def kernel_name(wl, out_int8, int8_contract="q14", coeff_table="on"):
     """The launch's dominant kernel (bf_fused.hip dispatch): item kernels for A <= 64 and T <= 256, else the wide
     kernels; the int8 32-beam path with a coefficient table (A <= 256) is the table-driven contraction, after its
@@ -579,7 +595,8 @@ def secondary(args, dist, workload, out_int8, int8_contract="q14"):
            "unit": "Gsamples/s", "n_gpus": dist.world,
            "roofline_frac": round(r["alg_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
            "read_frac": round(r["read_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
-           "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"]}
+           "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"],
+           "mfma": mfma_util(wl, out_int8, int8_contract, r["kernel_s"])}
     if not args.no_ceiling and dist.world == 1:
         ceil = stream_ceiling(args, r["read_bytes"], int(r["alg_bytes"] - r["read_bytes"]))
         if ceil:
@@ -697,6 +714,7 @@ def main():
                 e = rocprof_entry(regions, i + 1, s["kernel"], s["alg_bytes_per_launch"])
                 if e:
                     s["rocprof"] = e
+                    mfma_split(s, e)
     if dist.rank == 0 and dist.world == 1 and not args.no_pmc:
         try:
             traffic, info = pmc_traffic(args)

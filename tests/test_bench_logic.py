@@ -74,3 +74,27 @@ def test_timed_regions_keep_only_the_bracketed_dispatches(tmp_path):
     with open(out) as f:
         got = list(csv.DictReader(f))
     assert [(r["Region"], r["Name"]) for r in got] == [("0", "k_a"), ("0", "gen"), ("1", "k_b")]
+
+
+def test_mfma_block_and_contraction_split():
+    """Every line's mfma block: algorithmic ops 8 A M per (b, p, c, t), issued ops two limbs x K = 2A (padded to the
+    MFMA depth) x N = 2M (padded to 16); a two-kernel step (config 4's int8 path) also reports the contraction's own
+    rates over its rocprof time and the generator's share of the step."""
+    wl = bench.WORKLOADS["cfg4"]
+    m = bench.mfma_util(wl, True, "q14", 464e-6)
+    alg = 8.0 * 256 * 64 * 2 * 4096 * 256 * 1
+    assert m["algorithmic"] == pytest.approx(alg / 464e-6 / 1e12, abs=0.1)
+    assert m["issued"] == pytest.approx(2 * alg / 464e-6 / 1e12, abs=0.1)  # K, N unpadded here: 2 limbs = 2x
+    assert m["peak"] == 5000.0 and m["unit"] == "TOPS"
+    sec = {"avg_launch_us": 464.0, "mfma": m}
+    bench.mfma_split(sec, {"avg_us": 398.0, "per_step_us_all_kernels": 463.0,
+                           "kernels_us_per_step": {"w32t": 398.0, "q14_table_kernel<false>": 65.0}})
+    c = sec["mfma"]["contraction_only"]
+    assert c["kernel_us"] == 398.0
+    assert c["issued"] == pytest.approx(m["issued"] * 464.0 / 398.0, abs=0.2)
+    assert sec["mfma"]["generator_share_of_step"] == pytest.approx(65.0 / 463.0, abs=1e-3)
+    f = bench.mfma_util(wl, False, "q14", 620e-6)  # float beams: f16 hi/lo on the dense F16 peak
+    assert f["peak"] == 2500.0 and f["unit"] == "TFLOP/s"
+    one = {"avg_launch_us": 620.0, "mfma": f}
+    bench.mfma_split(one, {"avg_us": 620.0})  # one kernel per step: nothing to split
+    assert "contraction_only" not in one["mfma"]
