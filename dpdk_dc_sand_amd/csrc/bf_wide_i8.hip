@@ -1398,6 +1398,12 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
                 (prow + static_cast<uint32_t>(2 * (wave + 4 * pass) * 16 + i)) * static_cast<uint32_t>(M2) +
                     static_cast<uint32_t>(2 * m0),
                 0);
+            // Two wait states before any VALU may rewrite the store's data VGPRs: hipcc scheduled a write of its 4th
+            // data register right behind this store, and that dword of lanes 12-15 of every row went out wrong
+            // (~1e-5 of the bytes, run to run; tools/diag_w32r.py, tools/store_hazard_check.py).
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 1");
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
       }

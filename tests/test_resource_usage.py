@@ -62,3 +62,20 @@ def test_no_scratch_in_any_product_kernel(usage):
 def test_no_compiler_warnings_in_product_sources(usage):
     warnings = [w for _, (_, ws) in usage.items() for w in ws]
     assert not warnings, "\n".join(warnings[:20])
+
+
+def test_no_wide_store_data_hazard_in_product_kernels():
+    """No product kernel lets a VALU rewrite a wide store's data VGPRs right behind the store (tools/
+    store_hazard_check.py: the gfx950 store-data hazard hipcc left unguarded once, wrong bytes ~1e-5 of the time)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import store_hazard_check as shc
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        isas = dict(zip(SOURCES, ex.map(lambda s: shc.compile_isa(os.path.join(CSRC, s)), SOURCES)))
+    bad = []
+    for src, asm in isas.items():
+        total, hits = shc.scan(asm, window=2)
+        bad += [f"{src}: {fn[:90]}: {st} / {n}" for fn, st, n, _ in hits]
+    assert not bad, "\n".join(bad[:20])

@@ -1,0 +1,74 @@
+"""The store-data hazard of wide vector stores on gfx950: a VALU write to a VGPR that a just-issued dwordx3/x4 store
+still reads as data corrupts what that store writes for the last lanes it reads.  hipcc (ROCm 7.2) does not always
+keep the two apart: round 5 found a `buffer_store_dwordx4 v[80:83]` followed at once by a write of v83, and the 4th
+dword of lanes 12-15 of every row went out wrong in ~1e-5 of the bytes, varying run to run (tools/diag_w32r.py) --
+also the signature of round 4's unexplained w64h race.  This scans a source's device ISA for a VALU (or permlane
+swap) writing a wide store's data VGPRs within `window` instructions of it.
+usage: python tools/store_hazard_check.py <file.hip> [window] [extra hipcc flags]"""
+import re
+import subprocess
+import sys
+
+
+def _regs(tok):
+    m = re.match(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+def scan(asm, window=2):
+    """(wide stores, [(function, store, offending instruction, distance)]) of a device .s text."""
+    fn, lines = None, []
+    for line in asm.splitlines():
+        t = line.strip()
+        m = re.match(r"^(_Z\w+):", t)
+        if m:
+            fn = m.group(1)
+            continue
+        if not t or t.startswith((".", ";")) or t.endswith(":"):
+            continue
+        lines.append((fn, t))
+    total, hits = 0, []
+    for i, (fn, t) in enumerate(lines):
+        op = t.split()[0]
+        if not re.match(r"(buffer|global|flat)_store_dwordx[34]", op):
+            continue
+        total += 1
+        ops = [x.rstrip(",") for x in t.split()[1:]]
+        data = _regs(ops[0] if op.startswith("buffer") else ops[1])
+        for j in range(1, window + 1):
+            if i + j >= len(lines) or lines[i + j][0] != fn:
+                break
+            n = lines[i + j][1]
+            nop = n.split()[0]
+            if nop.startswith("s_nop"):
+                break  # s_nop k is k + 1 wait states: enough for this window
+            if nop.startswith("v_") and not nop.startswith("v_mfma"):
+                parts = [x.rstrip(",") for x in n.split()[1:]]
+                dst = _regs(parts[0]) if parts else set()
+                if "swap" in nop and len(parts) > 1:
+                    dst |= _regs(parts[1])
+                if dst & data:
+                    hits.append((fn, t, n, j))
+                    break
+    return total, hits
+
+
+def compile_isa(src, flags=()):
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-x", "hip", "-S",
+                        "--cuda-device-only", src, "-o", "-"] + list(flags), capture_output=True, text=True,
+                       timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr[-2000:])
+    return r.stdout
+
+
+if __name__ == "__main__":
+    window = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    total, hits = scan(compile_isa(sys.argv[1], sys.argv[3:]), window)
+    print(f"{total} wide stores, {len(hits)} with a VALU rewriting their data within {window} instructions")
+    for fn, t, n, j in hits[:40]:
+        name = subprocess.run(["c++filt", fn], capture_output=True, text=True).stdout.strip()[:90]
+        print(f"  {name}\n    {t}\n    +{j}: {n}")
