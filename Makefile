@@ -6,10 +6,10 @@ CSRC     := dpdk_dc_sand_amd/csrc
 LIB      := dpdk_dc_sand_amd/libbf.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -munsafe-fp-atomics
 SRCS     := $(CSRC)/bf_runtime.cpp $(CSRC)/bf_coeff.hip $(CSRC)/bf_reorder.hip $(CSRC)/bf_beamform.hip \
-            $(CSRC)/bf_fused.hip $(CSRC)/bf_wide.hip $(CSRC)/bf_wide_i8.hip $(CSRC)/bf_wide_i8os.hip $(CSRC)/bf_q14table.hip $(CSRC)/bf_requant.hip \
+            $(CSRC)/bf_fused.hip $(CSRC)/bf_wide.hip $(CSRC)/bf_wide_i8.hip $(CSRC)/bf_q14table.hip $(CSRC)/bf_requant.hip \
             $(CSRC)/bf_pipeline.cpp $(CSRC)/bf_comm.cpp
 OBJS     := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
-HDRS     := $(wildcard $(CSRC)/*.hpp) include/bf.h
+HDRS     := $(wildcard $(CSRC)/*.hpp) $(wildcard $(CSRC)/diag/*.inc) include/bf.h
 
 .PHONY: all clean diag cabi
 all: $(LIB) cabi
@@ -40,12 +40,15 @@ $(LIB): $(OBJS)
 clean:
 	rm -rf build $(LIB)
 
-# Diagnostic build (ablation variants + HBM stream kernel); used only by tools/diag_*.py, never by the product.
+# Diagnostic build (ablation variants + HBM stream kernel); used only by tools/diag_*.py and bench.py's stream
+# ceiling, never by the product.  The measured-slower kernels and the measurement entry points live in
+# $(CSRC)/diag/ (*.inc included under -DBF_DIAG, and the diagnostic-only bf_wide_i8os.hip).
 DIAG_LIB := build/libbf_diag.so
-DIAG_OBJS := $(patsubst $(CSRC)/%,build/diag/%.o,$(SRCS))
+DIAG_SRCS := $(SRCS) $(CSRC)/diag/bf_wide_i8os.hip
+DIAG_OBJS := $(patsubst $(CSRC)/%,build/diag/%.o,$(DIAG_SRCS))
 diag: $(DIAG_LIB)
 build/diag/%.o: $(CSRC)/% $(HDRS)
-	@mkdir -p build/diag
+	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -DBF_DIAG -x hip -c $< -o $@
 $(DIAG_LIB): $(DIAG_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(DIAG_OBJS) -ldl

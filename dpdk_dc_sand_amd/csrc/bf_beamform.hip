@@ -819,61 +819,5 @@ extern "C" int bf_beamform(const uint8_t* x, const float* w, float* y, int B, in
 }
 
 #ifdef BF_DIAG
-// Diagnostics: ablation of the MatrixMultiply ring kernel at a 256-antenna shape (tools/diag_fused.py,
-// DIAG_KERNELS=table): NTS 2 (two workgroups per CU) or 4 (one), R = 16; mode = the kernel's Mode bits.
-extern "C" int bf_diag_table(int mode, int nts, const uint8_t* x, const float* w, float* y, int B, int P, int C,
-                             int NB, int A, int M, void* stream) {
-  const int S = (2 * A + 31) / 32, NT = (2 * M + 15) / 16;
-  const long long bpc = static_cast<long long>(B) * P * C;
-  hipStream_t st = bf::as_stream(stream);
-#define BF_TABLE_MODE(m)                                                                                      \
-  case m:                                                                                                     \
-    return nts == 4 ? bf::launch_ring<true, 4, 16, m>(x, w, y, bpc, NB, A, M, S, NT, st)                      \
-                    : bf::launch_ring<true, 2, 16, m>(x, w, y, bpc, NB, A, M, S, NT, st)
-  switch (mode) {
-    BF_TABLE_MODE(0);
-    BF_TABLE_MODE(1);
-    BF_TABLE_MODE(2);
-    BF_TABLE_MODE(4);
-    BF_TABLE_MODE(8);
-    BF_TABLE_MODE(9);
-    BF_TABLE_MODE(6);
-    BF_TABLE_MODE(7);
-    case 200:  // the persistent form (A/B against mode 0); 200 + Mode bits: 1 no LDS staging, 4 no stores,
-               // 8 no x loads, 16 no table loads
-      return nts == 2 ? bf::launch_persist<true, 2, 16, 8>(x, w, y, bpc, NB, A, M, S, NT, st) : BF_ERR_ARG;
-    case 201: return bf::launch_persist<true, 2, 16, 8, 1>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 204: return bf::launch_persist<true, 2, 16, 8, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 208: return bf::launch_persist<true, 2, 16, 8, 8>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 216: return bf::launch_persist<true, 2, 16, 8, 16>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 217: return bf::launch_persist<true, 2, 16, 8, 17>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 220: return bf::launch_persist<true, 2, 16, 8, 20>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 228: return bf::launch_persist<true, 2, 16, 8, 28>(x, w, y, bpc, NB, A, M, S, NT, st);
-    // the output-stationary kernel (+ Mode bits)
-    case 400: return bf::launch_table_os<true, 0, 8>(x, w, y, bpc, A, st);
-    case 404: return bf::launch_table_os<true, 4, 8>(x, w, y, bpc, A, st);
-    case 408: return bf::launch_table_os<true, 8, 8>(x, w, y, bpc, A, st);
-    case 416: return bf::launch_table_os<true, 16, 8>(x, w, y, bpc, A, st);
-    case 428: return bf::launch_table_os<true, 28, 8>(x, w, y, bpc, A, st);
-    case 500: return bf::launch_table_os<true, 0, 4>(x, w, y, bpc, A, st);
-    case 600: return bf::launch_table_os<true, 0, 8, 3>(x, w, y, bpc, A, st);  // 8 waves, <= 168 VGPRs, 1 WG/CU
-    case 528: return bf::launch_table_os<true, 28, 4>(x, w, y, bpc, A, st);
-    // four row groups per pass (each LDS coefficient fragment feeds 8 MFMAs instead of 4), ring depth 8
-    case 240: return bf::launch_persist<true, 2, 8, 8, 0, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 268: return bf::launch_persist<true, 2, 8, 8, 28, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 250: return bf::launch_persist<true, 2, 16, 8, 0, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 278: return bf::launch_persist<true, 2, 16, 8, 28, 4>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 300:  // the non-persistent 16-byte ring
-      return nts == 4 ? bf::launch_ring<true, 4, 16>(x, w, y, bpc, NB, A, M, S, NT, st)
-                      : bf::launch_ring<true, 2, 16>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 100:  // the 8-byte-load form (A/B against mode 0)
-      return nts == 4 ? bf::launch_ring<true, 4, 16, 0, 1>(x, w, y, bpc, NB, A, M, S, NT, st)
-                      : bf::launch_ring<true, 2, 16, 0, 1>(x, w, y, bpc, NB, A, M, S, NT, st);
-    case 108:
-      return nts == 4 ? bf::launch_ring<true, 4, 16, 8, 1>(x, w, y, bpc, NB, A, M, S, NT, st)
-                      : bf::launch_ring<true, 2, 16, 8, 1>(x, w, y, bpc, NB, A, M, S, NT, st);
-    default: return BF_ERR_ARG;
-  }
-#undef BF_TABLE_MODE
-}
+#include "diag/beamform_diag.inc"
 #endif

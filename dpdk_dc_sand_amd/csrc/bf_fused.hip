@@ -1350,284 +1350,5 @@ extern "C" double bf_fused_algorithmic_bytes(int B, int C, int T, int A, int M, 
 }
 
 #ifdef BF_DIAG
-namespace bf {
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-// Streams in_bytes in and out_bytes out with 16-byte lanes, `unroll` loads in flight per lane before the stores:
-// the achievable HBM ceiling for the fused kernel's traffic mix.
-template <int U, bool NtLoad = false, bool NtStore = false>
-__global__ __launch_bounds__(256) void stream_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n_in,
-                                                     size_t n_out) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  const size_t n = n_in > n_out ? n_in : n_out;
-  for (size_t i0 = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i0 < n; i0 += stride * U) {
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const size_t i = i0 + u * stride;
-      if (i < n_in) {
-        if constexpr (NtLoad) {
-          const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + i));
-          v[u] = make_uint4(t[0], t[1], t[2], t[3]);
-        } else {
-          v[u] = in[i];
-        }
-      } else {
-        v[u] = make_uint4(static_cast<uint32_t>(i), 1, 2, 3);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const size_t i = i0 + u * stride;
-      if (i < n_out) {
-        if constexpr (NtStore) {
-          __builtin_nontemporal_store(u32x4{v[u].x, v[u].y, v[u].z, v[u].w}, reinterpret_cast<u32x4*>(out + i));
-        } else {
-          out[i] = v[u];
-        }
-      }
-    }
-  }
-}
-// The int8 path's traffic mix as a stream: 4 bytes read per byte written, uniformly over time (out[i] = xor of
-// four in-streams), non-temporal loads (and stores when NtStore).
-template <bool NtStore>
-__global__ __launch_bounds__(256) void stream_mix_kernel(const uint4* __restrict__ in, uint4* __restrict__ out,
-                                                         size_t n_out) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_out; i += stride) {
-    u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + i));
-#pragma unroll
-    for (int u = 1; u < 4; ++u) a ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + i + u * n_out));
-    if constexpr (NtStore)
-      __builtin_nontemporal_store(a, reinterpret_cast<u32x4*>(out + i));
-    else
-      *reinterpret_cast<u32x4*>(out + i) = a;
-  }
-}
-// The wide kernels' read pattern as a stream: the voltages (A, C, T*4) = rows of R = T*4 bytes per (antenna,
-// channel); item c needs row c of every antenna (stride C*R).  Pattern 0: one wave-load = one 1 KiB row piece,
-// the WG's waves take every 4th antenna; 1: w8's shape (16 lanes x 16 B of 4 antennas per wave-load); 2: a WG
-// owns `run` consecutive items and sweeps antenna-major (16 KiB contiguous per antenna at run 16).  U 16-byte loads
-// in flight per lane.  Items: the WG's `items` = C / grid.
-template <int Pattern, int U>
-__global__ __launch_bounds__(256) void item_read_kernel(const uint8_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                        int A, int C, int R) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const size_t astride = static_cast<size_t>(C) * R;
-  const int per = C / gridDim.x;
-  u32x4 acc = {0, 0, 0, 0};
-  if constexpr (Pattern == 2) {
-    const int c0 = blockIdx.x * per;  // rows c0 .. c0 + per - 1 of each antenna are contiguous
-    const size_t span = static_cast<size_t>(per) * R / 16;  // 16-byte pieces per antenna
-    const size_t n = span * A;
-    for (size_t i0 = threadIdx.x; i0 < n; i0 += 256 * U) {
-      u32x4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const size_t i = min(i0 + 256 * u, n - 1);
-        const size_t a = i / span, j = i % span;
-        v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + a * astride + static_cast<size_t>(c0) * R) + j);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) acc ^= v[u];
-    }
-  } else {
-    for (int k = 0; k < per; ++k) {
-      const int c = k * gridDim.x + blockIdx.x;
-      const uint8_t* item = in + static_cast<size_t>(c) * R;
-      const int rows_per_load = Pattern == 0 ? 1 : 4;
-      const int pieces = R / (Pattern == 0 ? 1024 : 256);  // per row
-      // load index L covers (antenna group, piece): 4 waves interleave
-      const int nloads = A / rows_per_load * pieces;
-      for (int l0 = wave; l0 < nloads; l0 += 4 * U) {
-        u32x4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int l = min(l0 + 4 * u, nloads - 1);
-          const int ag = l / pieces, pc = l % pieces;
-          size_t off;
-          if constexpr (Pattern == 0)
-            off = static_cast<size_t>(ag) * astride + pc * 1024 + lane * 16;
-          else
-            off = static_cast<size_t>(ag * 4 + (lane >> 4)) * astride + pc * 256 + (lane & 15) * 16;
-          v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(item + off));
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc ^= v[u];
-      }
-    }
-  }
-  const uint32_t s = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
-  if (s == 0x9e3779b9u) out[blockIdx.x * 256 + threadIdx.x] = s;
-}
-}  // namespace bf
-
-// code = 10 * pattern + (U == 16 ? 2 : U == 8 ? 1 : 0) (U = 4, 8, 16); the voltages' shape (A, C, R).
-extern "C" int bf_diag_item_read(const void* in, void* out, int A, int C, int R, int grid, int code, void* stream) {
-  auto i8 = reinterpret_cast<const uint8_t*>(in);
-  auto o = reinterpret_cast<uint32_t*>(out);
-  hipStream_t st = bf::as_stream(stream);
-  switch (code) {
-#define BF_IR(P, UI, U)                                                                                        \
-  case 10 * P + UI:                                                                                            \
-    hipLaunchKernelGGL((bf::item_read_kernel<P, U>), dim3(grid), dim3(256), 0, st, i8, o, A, C, R); \
-    break;
-    BF_IR(0, 0, 4) BF_IR(0, 1, 8) BF_IR(0, 2, 16) BF_IR(1, 0, 4) BF_IR(1, 1, 8) BF_IR(1, 2, 16) BF_IR(2, 0, 4)
-    BF_IR(2, 1, 8) BF_IR(2, 2, 16)
-#undef BF_IR
-    default: return BF_ERR_ARG;
-  }
-  BF_LAUNCHED("item_read_kernel");
-}
-
-extern "C" int bf_diag_stream(const void* in, void* out, size_t in_bytes, size_t out_bytes, int grid, int unroll,
-                              void* stream) {
-  auto in4 = reinterpret_cast<const uint4*>(in);
-  auto out4 = reinterpret_cast<uint4*>(out);
-  if (unroll == 200 || unroll == 201) {  // the 4:1 read:write mix (out_bytes = in_bytes / 4)
-    if (unroll == 200)
-      hipLaunchKernelGGL((bf::stream_mix_kernel<true>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
-                         out_bytes / 16);
-    else
-      hipLaunchKernelGGL((bf::stream_mix_kernel<false>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
-                         out_bytes / 16);
-    BF_LAUNCHED("stream_mix_kernel");
-  }
-  if (unroll == 101)
-    hipLaunchKernelGGL((bf::stream_kernel<1, false, true>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
-                       in_bytes / 16, out_bytes / 16);
-  else if (unroll == 102)
-    hipLaunchKernelGGL((bf::stream_kernel<1, true, false>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
-                       in_bytes / 16, out_bytes / 16);
-  else if (unroll == 103)
-    hipLaunchKernelGGL((bf::stream_kernel<1, true, true>), dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4,
-                       in_bytes / 16, out_bytes / 16);
-  else if (unroll >= 8)
-    hipLaunchKernelGGL(bf::stream_kernel<8>, dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4, in_bytes / 16,
-                       out_bytes / 16);
-  else if (unroll >= 4)
-    hipLaunchKernelGGL(bf::stream_kernel<4>, dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4, in_bytes / 16,
-                       out_bytes / 16);
-  else
-    hipLaunchKernelGGL(bf::stream_kernel<1>, dim3(grid), dim3(256), 0, bf::as_stream(stream), in4, out4, in_bytes / 16,
-                       out_bytes / 16);
-  BF_LAUNCHED("stream_kernel");
-}
-
-// Ablations of the item kernels (signed input, full tiles): mode 32 + kSkip* bits = the float item kernel (f32 beams,
-// fast coefficients), 512 + bits = the integer item kernel.
-extern "C" int bf_diag_fused(int mode, const uint8_t* raw, const float* dv, void* y, int B, int C, int T, int A, int M,
-                             int Ctot, double ts, void* stream) {
-  bf::FusedArgs P{};
-  P.raw = raw;
-  P.dv = reinterpret_cast<const float4*>(dv);
-  P.y = y;
-  P.delay_channels = 1;
-  P.B = B;
-  P.C = C;
-  P.T = T;
-  P.A = A;
-  P.M = M;
-  P.S = (2 * A + 31) / 32;
-  P.NT = (2 * M + 15) / 16;
-  P.ctot = Ctot;
-  P.ts = ts;
-  P.k = -3.141592653589793 / (Ctot * ts);
-  P.batch_dt = 1e-3;
-  P.out_scale = 1.0f;
-  hipStream_t st = bf::as_stream(stream);
-  BF_REQUIRE(P.S <= bf::kGroup && T <= 256 && (2 * M) % 32 == 0, "diag: item-kernel full-tile shapes only");
-  if (mode >= 16384) {  // float beams through the staged 1 KiB stores (kLdsStoreF32) + the item modes
-    switch (mode - 16384) {
-      case 0: return bf::launch_item<true, false, 2, false, true, bf::kLdsStoreF32>(P, st);
-      case 4: return bf::launch_item<true, false, 2, false, true, bf::kLdsStoreF32 | 4>(P, st);
-      case 128: return bf::launch_item<true, false, 2, false, true, bf::kLdsStoreF32 | 128>(P, st);
-      case 256: return bf::launch_item<true, false, 2, false, true, bf::kLdsStoreF32 | 256>(P, st);
-      case 384: return bf::launch_item<true, false, 2, false, true, bf::kLdsStoreF32 | 384>(P, st);
-      case 128 + 64: return bf::launch_item<true, false, 2, false, true, bf::kLdsStoreF32 | 128, 3>(P, st);
-      default: bf::set_error("bad mode"); return BF_ERR_ARG;
-    }
-  }
-  if (mode >= 8192) {  // int8 beams requantised from the float32 path (int8_contract = f32): the float item kernel
-    P.out_scale = 1.0f / 64;
-    switch (mode - 8192) {
-      case 0: return bf::launch_item<true, true, 2, false, true, 0>(P, st);
-      case 1: return bf::launch_item<true, true, 2, false, true, 1>(P, st);
-      case 2: return bf::launch_item<true, true, 2, false, true, 2>(P, st);
-      case 4: return bf::launch_item<true, true, 2, false, true, 4>(P, st);
-      case 5: return bf::launch_item<true, true, 2, false, true, 5>(P, st);
-      case 8: return bf::launch_item<true, true, 2, false, true, 8>(P, st);
-      case 128: return bf::launch_item<true, true, 2, false, true, 128>(P, st);
-      case 64: return bf::launch_item<true, true, 2, false, true, 0, 4>(P, st);
-      case 96: return bf::launch_item<true, true, 2, false, true, 0, 3>(P, st);
-      case 16: return bf::launch_item<true, true, 2, true, true, 0, 4>(P, st);  // exact coefficients (product occ)
-      case 80: return bf::launch_item<true, true, 2, true, true, 0, 1>(P, st);  // exact, unbounded
-      default: bf::set_error("bad mode"); return BF_ERR_ARG;
-    }
-  }
-  if (mode >= 512) {  // integer (int8-output) item kernel
-    P.out_scale = 1.0f / 64;
-    switch (mode - 512) {
-      case 0: return bf::launch_i8_item<true, 2, true, 0>(P, st);
-      case 1: return bf::launch_i8_item<true, 2, true, 1>(P, st);
-      case 2: return bf::launch_i8_item<true, 2, true, 2>(P, st);
-      case 3: return bf::launch_i8_item<true, 2, true, 3>(P, st);
-      case 4: return bf::launch_i8_item<true, 2, true, 4>(P, st);
-      case 5: return bf::launch_i8_item<true, 2, true, 5>(P, st);
-      case 7: return bf::launch_i8_item<true, 2, true, 7>(P, st);
-      case 8: return bf::launch_i8_item<true, 2, true, 8>(P, st);
-      case 16: return bf::launch_i8_item<true, 2, true, 16>(P, st);
-      case 128: return bf::launch_i8_item<true, 2, true, 128>(P, st);
-      case 32: return bf::launch_i8_item<true, 2, true, 32>(P, st);
-      case 64: return bf::launch_i8_item<true, 2, true, 0>(P, st, 60 * 1024);  // occupancy 2 (LDS-limited)
-      case 65: return bf::launch_i8_item<true, 2, true, 4>(P, st, 60 * 1024);
-      // layout variants: serial coefficients, pol order, both; 4 waves per SIMD (spills), 3 (the product's bound)
-      case 1024: return bf::launch_i8_item<true, 2, true, 1024>(P, st);
-      case 2048: return bf::launch_i8_item<true, 2, true, 2048>(P, st);
-      case 3072: return bf::launch_i8_item<true, 2, true, 3072>(P, st);
-      case 4096: return bf::launch_i8_item<true, 2, true, 0, 4>(P, st);
-      case 4096 + 3072: return bf::launch_i8_item<true, 2, true, 3072, 4>(P, st);
-      case 4096 + 2048: return bf::launch_i8_item<true, 2, true, 2048, 4>(P, st);
-      case 262144: return bf::launch_i8_item<true, 2, true, 262144>(P, st);
-      case 524288: return bf::launch_i8_item<true, 2, true, 524288>(P, st);
-      case 4194304: return bf::launch_i8_item<true, 2, true, 4194304>(P, st);
-      case 8388608: return bf::launch_i8_item<true, 2, true, 8388608>(P, st);
-      case 1048576: return bf::launch_i8_item<true, 2, true, 1048576>(P, st);
-      case 2097152: return bf::launch_i8_item<true, 2, true, 2097152>(P, st);  // channel fastest (earlier order)
-      case 65536: return bf::launch_i8_item<true, 2, true, 65536>(P, st);
-      case 131072: return bf::launch_i8_item<true, 2, true, 131072>(P, st);
-      case 8192: return bf::launch_i8_item<true, 2, true, 8192>(P, st);
-      case 16384: return bf::launch_i8_item<true, 2, true, 16384>(P, st);
-      case 8192 + 16384: return bf::launch_i8_item<true, 2, true, 8192 + 16384>(P, st);
-      default: bf::set_error("bad mode"); return BF_ERR_ARG;
-    }
-  }
-  if (mode >= 32) {
-    switch (mode - 32) {
-      case 0: return bf::launch_item<true, false, 2, false, true, 0>(P, st);
-      case 1: return bf::launch_item<true, false, 2, false, true, 1>(P, st);
-      case 2: return bf::launch_item<true, false, 2, false, true, 2>(P, st);
-      case 3: return bf::launch_item<true, false, 2, false, true, 3>(P, st);
-      case 4: return bf::launch_item<true, false, 2, false, true, 4>(P, st);
-      case 5: return bf::launch_item<true, false, 2, false, true, 5>(P, st);
-      case 7: return bf::launch_item<true, false, 2, false, true, 7>(P, st);
-      case 8: return bf::launch_item<true, false, 2, false, true, 8>(P, st);
-      case 9: return bf::launch_item<true, false, 2, false, true, 9>(P, st);
-      case 11: return bf::launch_item<true, false, 2, false, true, 11>(P, st);
-      case 16: return bf::launch_item<true, false, 2, true, true, 0>(P, st);
-      case 128: return bf::launch_item<true, false, 2, false, true, 128>(P, st);
-      case 256: return bf::launch_item<true, false, 2, false, true, 256>(P, st);
-      case 384: return bf::launch_item<true, false, 2, false, true, 384>(P, st);
-      case 64: return bf::launch_item<true, false, 2, false, true, 0, 4>(P, st);  // 4 waves per SIMD bound
-      case 96: return bf::launch_item<true, false, 2, false, true, 0, 3>(P, st);  // 3 waves per SIMD bound
-      case 160: return bf::launch_item<true, false, 2, false, true, 512>(P, st);  // channel-fastest order
-      case 192: return bf::launch_item<true, false, 2, false, true, 1024>(P, st);  // batch-fastest order
-      case 224: return bf::launch_item<true, false, 2, false, true, 2048>(P, st);  // XCD x batch order
-      case 288: return bf::launch_item<true, false, 2, false, true, 256>(P, st);  // nt stores
-      default: bf::set_error("bad mode"); return BF_ERR_ARG;
-    }
-  }
-  bf::set_error("bad mode");
-  return BF_ERR_ARG;
-}
-#endif  // BF_DIAG
+#include "diag/fused_diag.inc"
+#endif

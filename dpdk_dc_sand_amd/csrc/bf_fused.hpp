@@ -123,9 +123,12 @@ __host__ __device__ inline int w32h_item_words(int Sp) { return 1024 * Sp + kW32
 __host__ __device__ inline int w32_table_steps(int A) { return 4 * ((((A + 31) >> 5) + 3) / 4); }
 // The table-driven 32-beam kernel stages at most 4 units of 8 words per thread: Sp <= 8 (A <= 256).
 __host__ __device__ inline bool w32_table_fits(int A) { return w32_table_steps(A) <= 8; }
-// Bytes of the int8 wide path's coefficient table of one launch: w32h_item_words(Sp) words per (b, c, 32-beam slab)
-// (kLayoutW32 uses the first 1024 Sp of them).
+// Bytes of the int8 wide path's coefficient table of one launch (kLayoutW32): 1024 Sp words per (b, c, 32-beam slab).
 inline size_t w32_table_bytes(int B, int C, int A, int M) {
+  return static_cast<size_t>(B) * C * ((M + 31) / 32) * 1024 * w32_table_steps(A) * 4;
+}
+// The diagnostic halved-image layout (kLayoutW32H): w32h_item_words(Sp) words per (b, c, 32-beam slab).
+inline size_t w32h_table_bytes(int B, int C, int A, int M) {
   return static_cast<size_t>(B) * C * ((M + 31) / 32) * w32h_item_words(w32_table_steps(A)) * 4;
 }
 int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t st);

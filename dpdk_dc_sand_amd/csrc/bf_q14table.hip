@@ -148,129 +148,9 @@ __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
   }
 }
 
-// kLayoutW32H: the config-4 int8 contraction's halved limb image, written in the exact byte order of its LDS image so
-// the contraction copies it in by LDS-DMA (bf_wide_i8.hip, beamform_fused_i8_w32h_kernel).  Per (b, c, slab) word
-//   ((s * 2 + t) * 2 + L) * 256 + lane * 4 + w,   lane = row + 16 h,
-// holds limb L (0 = hi, 1 = lo) of (Wc, -Ws) for beam 16 t + row of the slab and slot antennas 32 s + 8 h + 2 w + e
-// (e = 0, 1: bytes 2 e, 2 e + 1) -- one MFMA A-operand lane fragment per 16 bytes.  Balanced limbs: v = 256 hi + lo,
-// lo = v's low byte as int8, hi = (v + 128) >> 8.  After the image, 2 words per beam: sum_a Wc, sum_a Ws (the
-// contraction's y_im uses [x_im, ~x_re], whose bias is sum_a Ws; unsigned samples also need the x - 128 sums).
-// Workgroup = 1024 threads = one (b, run of channels, slab, tile t): thread k owns beam row (k >> 2) & 15, lane group
-// h = (k >> 6) & 3, word w = k & 3 and the steps s = k >> 8 and s + 4 (Sp <= 8) -- 2 x 2 coefficients, each walked
-// along the run with the float64 recurrence of q14_table_kernel -- so a wave stores 256 contiguous bytes per
-// instruction and the column sums reduce inside the workgroup (a quad shuffle, then LDS atomics).
-template <bool Gain, bool PerCh>
-__global__ __launch_bounds__(1024) void q14_image_kernel(Q14TableArgs P) {
-  __shared__ int csum[kQ14Run][16][2];
-  const int t = blockIdx.x & 1, slab = blockIdx.x >> 1;
-  const int b = blockIdx.z;
-  const int c0 = blockIdx.y * P.run;
-  const int nrun = min(P.run, P.Cn - c0);
-  const int k = threadIdx.x, row = (k >> 2) & 15, h = (k >> 6) & 3, w = k & 3, sq = k >> 8;
-  const int m = slab * 32 + 16 * t + row;
-  for (int i = k; i < nrun * 32; i += 1024) (&csum[0][0][0])[i] = 0;
-  const size_t words = static_cast<size_t>(w32h_item_words(P.Sp)) * P.nslabs;  // per (b, c)
-  uint32_t* o = P.out + (static_cast<size_t>(b) * P.C + c0) * words + static_cast<size_t>(slab) * w32h_item_words(P.Sp);
-  const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
-  const double half = P.ctot / 2.0;
-  const int mm = min(m, P.M - 1);
-  __syncthreads();
-  // the thread's two positions one after the other (steps sq, then sq + 4), each a pair of coefficients (antenna e)
-  // walked along the run: half the live recurrence state of doing both at once (registers are the 1024-thread
-  // workgroup's limit)
-  for (int pi = 0; pi < 2; ++pi) {
-    const int s = sq + 4 * pi;
-    if (s >= P.Sp) break;  // uniform
-    int ant[2];  // -1: no coefficient (a covered slot antenna, a padded step, a beam past M)
-    double re[2], im[2], cd[2], sd[2];
-    float gq[2];  // gain * 2^14
-    bool in_range[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      int a = 0;
-      const bool valid = m < P.M && w32_slot_antenna(32 * s + 8 * h + 2 * w + e, P.A, &a);
-      ant[e] = valid ? a : -1;
-      const size_t am = static_cast<size_t>(mm) * P.A + max(ant[e], 0);
-      gq[e] = (Gain ? P.gain[am] : 1.0f) * 16384.0f;
-      re[e] = 16384.0, im[e] = 0.0, cd[e] = 1.0, sd[e] = 0.0;
-      in_range[e] = false;
-      if constexpr (!PerCh) {
-        const float4 dv = P.dv[am];
-        const double tau = fma(static_cast<double>(dv.y), dt, static_cast<double>(dv.x));
-        const double phi = fma(static_cast<double>(dv.w), dt, static_cast<double>(dv.z));
-        const double ch_last = static_cast<double>(P.base_ch + c0 + nrun - 1);
-        const float mag = fabsf(static_cast<float>(tau)) * static_cast<float>((ch_last + half) * fabs(P.k)) +
-                          fabsf(static_cast<float>(phi));
-        in_range[e] = mag < kQ14MaxMag;
-        if (in_range[e]) {
-          const double ch0 = static_cast<double>(P.base_ch + c0);
-          sincos_pio2(fma(tau * (ch0 - half), P.k, phi), &im[e], &re[e]);
-          sincos_pio2(tau * P.k, &sd[e], &cd[e]);
-          re[e] *= 16384.0;
-          im[e] *= 16384.0;
-        }
-      }
-    }
-    const int base = ((s * 2 + t) * 2) * 256 + (16 * h + row) * 4 + w;
-    for (int jc = 0; jc < nrun; ++jc) {
-      const int c = c0 + jc;
-      int wc[2], ws[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const size_t am = static_cast<size_t>(mm) * P.A + max(ant[e], 0);
-        if constexpr (PerCh) {  // a model per channel: a fast phasor per channel, exact where undecided
-          const float4 d = P.dv[static_cast<size_t>(c) * P.M * P.A + am];
-          const double ch = static_cast<double>(P.base_ch + c);
-          const float uk = static_cast<float>((ch + half) * fabs(P.k));
-          if (!q14_fast(d, ch - half, P.k, dt, uk, gq[e], &wc[e], &ws[e]))
-            q14_exact(d, ch, P.ctot, P.ts, dt, P.gain, gq[e] * 0x1p-14f, &wc[e], &ws[e]);
-        } else {
-          bool ok = in_range[e];
-          if (Gain || !P.unit_fast) {
-            wc[e] = q14_pair(re[e] * 0x1p-14, gq[e], &ok);
-            ws[e] = q14_pair(im[e] * 0x1p-14, gq[e], &ok);
-          } else {
-            wc[e] = q14_pair_unit_scaled(re[e], &ok);
-            ws[e] = q14_pair_unit_scaled(im[e], &ok);
-          }
-          if (!ok)  // (the model reloaded: rare)
-            q14_exact(P.dv[am], static_cast<double>(c + P.base_ch), P.ctot, P.ts, dt, P.gain, gq[e] * 0x1p-14f,
-                      &wc[e], &ws[e]);
-          const double r2 = fma(re[e], cd[e], -im[e] * sd[e]);
-          im[e] = fma(re[e], sd[e], im[e] * cd[e]);
-          re[e] = r2;
-        }
-        if (ant[e] < 0) wc[e] = ws[e] = 0;
-      }
-      // limbs of (Wc, -Ws) per antenna e as 16-bit lanes: lo = the low bytes, hi = byte 1 of v + 128 (no carry
-      // crosses the 16-bit halves)
-      const uint32_t v0 = (static_cast<uint32_t>(wc[0]) & 0xffffu) | (static_cast<uint32_t>(-ws[0]) << 16);
-      const uint32_t v1 = (static_cast<uint32_t>(wc[1]) & 0xffffu) | (static_cast<uint32_t>(-ws[1]) << 16);
-      const uint32_t lo = __builtin_amdgcn_perm(v1, v0, 0x06040200u);  // [Wc0.b0, nWs0.b0, Wc1.b0, nWs1.b0]
-      const uint32_t h0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, v0) + u16x2{128, 128});
-      const uint32_t h1 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, v1) + u16x2{128, 128});
-      const uint32_t hi = __builtin_amdgcn_perm(h1, h0, 0x07050301u);
-      uint32_t* oc = o + static_cast<size_t>(jc) * words + base;
-      oc[0] = hi;
-      oc[256] = lo;
-      int sc = wc[0] + wc[1], ss = ws[0] + ws[1];
-      sc += __shfl_xor(sc, 1);
-      ss += __shfl_xor(ss, 1);
-      sc += __shfl_xor(sc, 2);
-      ss += __shfl_xor(ss, 2);
-      if (w == 0) {
-        atomicAdd(&csum[jc][row][0], sc);
-        atomicAdd(&csum[jc][row][1], ss);
-      }
-    }
-  }
-  __syncthreads();
-  const int img = 1024 * P.Sp;
-  for (int i = k; i < nrun * 32; i += 1024) {  // channel i >> 5: beam 16 t + (i & 31) / 2, component i & 1
-    const int jc = i >> 5, r = i & 31;
-    o[static_cast<size_t>(jc) * words + img + 32 * t + r] = static_cast<uint32_t>(csum[jc][r >> 1][r & 1]);
-  }
-}
+#ifdef BF_DIAG
+#include "diag/q14_image.inc"  // the halved-image generator (diagnostic build only)
+#endif
 
 }  // namespace
 
@@ -295,6 +175,7 @@ int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t 
   Q.run = rn ? std::max(1, atoi(rn)) : kQ14Run;
   const char* uf = diag_env("BF_Q14_UNIT");  // measurement: 0 = the two-sided decision for unit gains too
   Q.unit_fast = !(uf && uf[0] == '0');
+#ifdef BF_DIAG
   if (layout == kLayoutW32H) {  // one 1024-thread workgroup per (b, run, slab, 16-beam tile)
     Q.run = std::min(Q.run, kQ14Run);
     const long long gy = (Q.Cn + Q.run - 1) / Q.run;
@@ -310,6 +191,9 @@ int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t 
       hipLaunchKernelGGL((q14_image_kernel<false, false>), grid, dim3(1024), 0, st, Q);
     BF_LAUNCHED("q14_image_kernel");
   }
+#else
+  BF_REQUIRE(layout != kLayoutW32H, "q14 table: the halved-image layout is in the diagnostic build only");
+#endif
   Q.run = std::min(Q.run, 64);  // (the deferred-fixup mask of q14_table_kernel holds 64 channels)
   const long long gx = (words + 255) / 256, gy = (Q.Cn + Q.run - 1) / Q.run;
   BF_REQUIRE(gx < (1LL << 31) && gy < 65536 && P.B < 65536, "q14 table: grid too large");

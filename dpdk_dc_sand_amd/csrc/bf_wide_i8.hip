@@ -1,6 +1,6 @@
 // Integer wide fused beamformer: many antennas x beams (config 4: 256 antennas, 64 beams), int8 beams, bit-exact.
-// The 32-beam slab kernels further down are the product (BF_FUSED_PATH_WIDE); the round-1 16-beam slab kernel here is
-// compiled in the diagnostic build only (BF_DIAG: tools/diag_fused.py ablations), as measured slower.
+// The 32-beam slab kernels are the product (BF_FUSED_PATH_WIDE); the measured-slower forms (the round-1 16-beam slabs,
+// round 4's halved-image kernel) and the measurement entry points live in diag/*.inc, compiled only with -DBF_DIAG.
 //
 // Same integer contract as beamform_fused_i8_item_kernel (oracle.fused_beamform_int8: Q14 coefficients of the
 // exact float32 phasors, exact int32 products, one float rounding to int8), organised like the float wide kernel
@@ -25,327 +25,9 @@ __device__ __forceinline__ int w8_step_base(int s, int A) { return min(32 * s, A
 // k-steps of 32 antennas, padded to an even count (ping-pong, see the float wide kernel)
 __host__ __device__ inline int w8_padded_steps(int A) { return 2 * ((((A + 31) >> 5) + 1) / 2); }
 
-#ifdef BF_DIAG  // the 16-beam slab kernel (diagnostic build only)
-constexpr int kW8Beams = 16;  // beams per workgroup slab (2 tiles of 16 real columns)
-
-// The item's voltages as a buffer resource (gfx9 raw-buffer descriptor word 3): every load is then
-// buffer_load_dwordx4 with the lane offset in a VGPR and the wave-uniform antenna offset in an SGPR -- no per-load
-// 64-bit address arithmetic on the VALU (3 instructions per load, one of them a v_mad_u64_u32, in the pointer form).
-// Needs every offset < 2^31 (the host checks A * C * T * 4); otherwise the pointer form is used.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t w8_rsrc(const uint8_t* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7fffffff, 0x00020000);
-}
-
-template <int Mode, bool Buf>
-__device__ __forceinline__ void w8_load(const uint8_t* __restrict__ base, __amdgpu_buffer_rsrc_t rsrc, size_t ant_stride,
-                                        uint32_t loff, int s, int A, uint32_t (&d)[8][4]) {
-  const int a0 = (Mode & 64) ? 8 * (s & 1) : w8_step_base(s, A);  // 64: diagnostics, 16 antenna rows only
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    if constexpr (Mode & 8) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) d[q][j] = loff * 0x01010101u + s + q + j;
-      continue;
-    }
-    u32x4_t v;
-    if constexpr ((Mode & 32) != 0)  // diagnostics: non-temporal loads
-      v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a0 + q) * ant_stride + loff));
-    else if constexpr (Buf)
-      v = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                          rsrc, loff, static_cast<uint32_t>(a0 + q) * static_cast<uint32_t>(ant_stride), 0));
-    else
-      v = *reinterpret_cast<const u32x4_t*>(base + static_cast<size_t>(a0 + q) * ant_stride + loff);
-    d[q][0] = v[0];
-    d[q][1] = v[1];
-    d[q][2] = v[2];
-    d[q][3] = v[3];
-  }
-}
-
-template <bool Signed, int Mode>
-__device__ __forceinline__ void w8_contract(const int4* __restrict__ fr, int s, int lane, const uint32_t (&d)[8][4],
-                                            i32x4_t (&hi)[2][4][2], i32x4_t (&lo)[2][4][2]) {
-  i32x4_t chi[2], clo[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int4 x0 = fr[(((s * 2 + t) * 2 + 0) * 64) + lane];
-    const int4 x1 = fr[(((s * 2 + t) * 2 + 1) * 64) + lane];
-    chi[t] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
-    clo[t] = i32x4_t{x1.x, x1.y, x1.z, x1.w};
-  }
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const uint32_t sel = p ? kSelP1 : kSelP0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      uint32_t w[4];
-#pragma unroll
-      for (int m2 = 0; m2 < 4; ++m2) {
-        uint32_t a = d[2 * m2][i], b = d[2 * m2 + 1][i];
-        if constexpr (!Signed) {  // x - 128 as int8 (128 * column sum added back at the end)
-          a ^= 0x80808080u;
-          b ^= 0x80808080u;
-        }
-        w[m2] = __builtin_amdgcn_perm(b, a, sel);
-      }
-      const i32x4_t f = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]),
-                                static_cast<int>(w[3])};
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        if constexpr (Mode & 2) {
-          hi[p][i][t] += f + chi[t];
-          lo[p][i][t] += f + clo[t];
-        } else {
-          hi[p][i][t] = mfma_i8(chi[t], f, hi[p][i][t]);
-          lo[p][i][t] = mfma_i8(clo[t], f, lo[p][i][t]);
-        }
-      }
-    }
-  }
-}
-
-// Mode (diagnostics only): 1 synthetic coefficients, 2 no MFMA, 4 no stores, 8 no voltage loads, 16 only the first
-// beam slab of each item works (each item's voltages read once), 32 non-temporal voltage loads.
-template <bool Signed, int Mode = 0, bool Buf = true>
-__global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_wide_kernel(FusedArgs P) {
-  extern __shared__ __attribute__((aligned(16))) int4 lds4[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 4, tl = lane & 15;
-  int slab, bc;
-  if constexpr ((Mode & 256) != 0) {  // diagnostics: XCD x streams the contiguous item range [x BC/8, (x+1) BC/8)
-    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
-    slab = local % P.nslabs;
-    bc = x * ((P.B * P.C) >> 3) + local / P.nslabs;
-    if (bc >= P.B * P.C) return;
-  } else if (P.xcd_order) {  // the slabs of one item back to back on one XCD: later slabs re-read from L2
-    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
-    slab = local % P.nslabs;
-    bc = (local / P.nslabs) * 8 + x;
-    if (bc >= P.B * P.C) return;
-  } else {
-    slab = blockIdx.x % P.nslabs;
-    bc = blockIdx.x / P.nslabs;
-  }
-  if constexpr ((Mode & 16) != 0)
-    if (slab != 0) return;
-  const int b = bc / P.C, c = bc % P.C;
-  const int m0 = slab * kW8Beams;
-  const int Sp = w8_padded_steps(P.A);
-  const int T4 = P.T >> 2;
-  const int npasses = (((T4 + 15) >> 4) + 3) >> 2;  // 64-sample chunks per wave, the same count for every wave
-  const size_t ant_stride = static_cast<size_t>(P.C) * P.T * 4;
-  const uint32_t hoff = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride);  // < 24 * stride
-  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * P.C + c) * static_cast<size_t>(P.T) * 4;
-  const __amdgpu_buffer_rsrc_t rsrc = w8_rsrc(base);
-  int8_t* lb = reinterpret_cast<int8_t*>(lds4);
-  int* partial = reinterpret_cast<int*>(lb + static_cast<size_t>(Sp) * 2 * 2 * 64 * 16);  // [4 waves][32 columns]
-
-  uint32_t d0[8][4], d1[8][4];
-  int chunk = wave;
-  uint32_t loff = hoff + static_cast<uint32_t>(min(chunk * 16 + tl, T4 - 1)) * 16u;
-  w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, 0, P.A, d0);
-  w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, 1, P.A, d1);
-
-  // Q14 limbs of the slab's [[R, I], [-I, R]] blocks for every slot antenna (exact float64 phasors), under the
-  // loads.  Pair e -> 4 consecutive slot antennas x beam row ml (ml is fixed per thread: the column sums of the
-  // unsigned correction reduce over the 4 lanes sharing it).
-  {
-    const double dt = P.t0 + static_cast<double>(b) * P.batch_dt;
-    const double ch = static_cast<double>(P.base_ch + c);
-    const int cd = P.delay_channels == 1 ? 0 : c;
-    const int npairs = 32 * Sp * kW8Beams;
-    int cs0 = 0, cs1 = 0;
-    // pair e = tid + 256 J of this thread: beam row ml = (tid >> 2) % 16 (the same for every J) and slot antenna
-    // sa0 + 16 J -- the per-pair index arithmetic reduces to one add
-    const int ml = (tid >> 2) & (kW8Beams - 1);
-    const int sa0 = 4 * (tid >> 6) + (tid & 3);
-    const int m = m0 + ml;
-    const bool m_ok = m < P.M;
-    const float4* dv_row = P.dv + (static_cast<size_t>(cd) * P.M + min(m, P.M - 1)) * P.A;
-    const float* g_row = P.gain ? P.gain + static_cast<size_t>(min(m, P.M - 1)) * P.A : nullptr;
-    const int nj = npairs / kW8Threads;  // 2 Sp
-    const int off0 = coef8_byte(2 * sa0, 2 * ml, 2, 0);
-    constexpr int kBatch = 8;
-    for (int j0 = 0; j0 < nj; j0 += kBatch) {
-      float4 dv[kBatch];
-      float gv[kBatch];
-      bool valid[kBatch];
-      int wc[kBatch], ws[kBatch];
-#pragma unroll
-      for (int j = 0; j < kBatch; ++j) {
-        const int sa = sa0 + 16 * (j0 + j), st = sa >> 5;
-        const int a = w8_step_base(st, P.A) + (sa & 31);
-        // rows of antennas an earlier step already covered stay zero
-        valid[j] = j0 + j < nj && m_ok && a >= 32 * st;
-        if constexpr (Mode & 1) continue;
-        dv[j] = dv_row[min(a, P.A - 1)];
-        gv[j] = g_row ? g_row[min(a, P.A - 1)] : 1.0f;
-      }
-      if constexpr (Mode & 1) {
-#pragma unroll
-        for (int j = 0; j < kBatch; ++j) {
-          wc[j] = 8192 + 16 * j + tid;
-          ws[j] = 4096 - 16 * j;
-        }
-      } else {
-        // branch-free fast phasors (the kBatch float64 chains interleave); Mode 512: the branchy form (diagnostics)
-        q14_coeffs<kBatch, !(Mode & 128), false, (Mode & 512) == 0>(dv, gv, valid, ch, P.ctot, P.ts, P.k, dt, P.gain,
-                                                                     wc, ws);
-      }
-#pragma unroll
-      for (int j = 0; j < kBatch; ++j) {
-        if (j0 + j >= nj) break;
-        const int J = j0 + j;
-        const int Wc = wc[j], Ws = ws[j], nWs = -Ws;
-        // Column 2 ml holds (k = 2 sa, 2 sa + 1) = (Wc, -Ws), column 2 ml + 1 holds (Ws, Wc): one 16-bit write per
-        // (column, limb).  Balanced limbs W = 256 hi + lo, lo in [-128, 127]: lo's byte is W's byte 0 and hi's byte
-        // is byte 1 of W + 128, so each pair of limb bytes is one v_perm.  Pair J's image offset is the thread's
-        // base plus a constant (k = 2 sa0 + 32 J with 2 sa0 < 32: step J >> 1, lane group + 2 (J & 1)).
-        int8_t* o = lb + off0 + 4096 * (J >> 1) + 512 * (J & 1);
-        *reinterpret_cast<uint16_t*>(o) = static_cast<uint16_t>(__builtin_amdgcn_perm(nWs + 128, Wc + 128, 0x0c0c0501u));
-        *reinterpret_cast<uint16_t*>(o + 64 * 16) = static_cast<uint16_t>(__builtin_amdgcn_perm(nWs, Wc, 0x0c0c0400u));
-        *reinterpret_cast<uint16_t*>(o + 16) = static_cast<uint16_t>(__builtin_amdgcn_perm(Wc + 128, Ws + 128, 0x0c0c0501u));
-        *reinterpret_cast<uint16_t*>(o + 16 + 64 * 16) = static_cast<uint16_t>(__builtin_amdgcn_perm(Wc, Ws, 0x0c0c0400u));
-        cs0 += Wc - Ws;  // column 2m:   W[2a][2m] + W[2a+1][2m]
-        cs1 += Ws + Wc;  // column 2m+1: W[2a][2m+1] + W[2a+1][2m+1]
-      }
-    }
-    if constexpr (!Signed) {
-      cs0 += __shfl_xor(cs0, 1);
-      cs1 += __shfl_xor(cs1, 1);
-      cs0 += __shfl_xor(cs0, 2);
-      cs1 += __shfl_xor(cs1, 2);
-      if ((lane & 3) == 0) {
-        partial[wave * 32 + 2 * (lane >> 2)] = cs0;
-        partial[wave * 32 + 2 * (lane >> 2) + 1] = cs1;
-      }
-    }
-  }
-  __syncthreads();
-
-  // unsigned samples: 128 * column sum for the lane's output columns 16 t + 4 h + r (sum of the 4 wave partials)
-  int corr[2][4];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      corr[t][r] = 0;
-      if constexpr (!Signed) {
-        const int cl = 16 * t + 4 * h + r;
-        corr[t][r] = 128 * (partial[cl] + partial[32 + cl] + partial[64 + cl] + partial[96 + cl]);
-      }
-    }
-  const float s32 = P.out_scale * 0x1p-14f;
-  const int M2 = 2 * P.M;
-  const bool full = m0 + kW8Beams <= P.M && (M2 & 15) == 0;  // 16-byte row pieces (uniform)
-
-  for (int pass = 0; pass < npasses; ++pass) {
-    const int tq = chunk * 16 + tl;
-    i32x4_t hi[2][4][2], lo[2][4][2];
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) hi[p][i][t] = lo[p][i][t] = i32x4_t{0, 0, 0, 0};
-      for (int s = 0; s < Sp; s += 2) {  // ping-pong, unconditional clamped prefetch (exact vmcnt, see bf_wide.hip)
-        w8_contract<Signed, Mode>(lds4, s, lane, d0, hi, lo);
-        w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, min(s + 2, Sp - 1), P.A, d0);
-        w8_contract<Signed, Mode>(lds4, s + 1, lane, d1, hi, lo);
-        w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, min(s + 3, Sp - 1), P.A, d1);
-      }
-    const int next = chunk + 4;
-    if (pass + 1 < npasses) {  // next chunk's first steps in flight during the stores
-      loff = hoff + static_cast<uint32_t>(min(next * 16 + tl, T4 - 1)) * 16u;
-      w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, 0, P.A, d0);
-      w8_load<Mode, Buf>(base, rsrc, ant_stride, loff, 1, P.A, d1);
-    }
-    if constexpr (Mode & 4) {
-      int sum = 0;
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) sum += hi[p][i][t][0] ^ lo[p][i][t][3];
-      if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[tid] = sum;
-    } else {
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        uint32_t pk[2][4];  // [tile][sample i] -> 4 packed int8 columns 16 t + 4 h + r
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            uint32_t qb[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              int y = (hi[p][i][t][r] << 8) + lo[p][i][t][r];
-              if constexpr (!Signed) y += corr[t][r];
-              qb[r] = requant_bits(y, s32);
-            }
-            pk[t][i] = pack_low_bytes(qb[0], qb[1], qb[2], qb[3]);
-          }
-        const size_t prow = ((static_cast<size_t>(b) * 2 + p) * P.C + c) * static_cast<size_t>(P.T);
-        if (full) {
-          // 4x4 transpose over (h, i): lane (tl, h) gets output row 4 tq + h, columns 16 t .. 16 t + 15 -> the slab's
-          // 32 bytes of the row as two 16-byte stores
-#pragma unroll
-          for (int t = 0; t < 2; ++t) transpose_rows4(pk[t]);
-          if (tq < T4) {
-            int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 4 * tq + h) * M2 + 2 * m0;
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-              *reinterpret_cast<u32x4_t*>(o + 16 * t) = u32x4_t{pk[t][0], pk[t][1], pk[t][2], pk[t][3]};
-          }
-        } else if (tq < T4) {  // partial slab / unaligned rows: byte stores with the beam guard
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            int8_t* o = reinterpret_cast<int8_t*>(P.y) + (prow + 4 * tq + i) * M2 + 2 * m0;
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int col = 16 * t + 4 * h + r;
-                if (2 * m0 + col < M2) o[col] = static_cast<int8_t>((pk[t][i] >> (8 * r)) & 255);
-              }
-          }
-        }
-      }
-    }
-    chunk = next;
-  }
-}
-
-template <bool Signed, int Mode = 0>
-int launch_w8(FusedArgs P, hipStream_t st) {
-  const int Sp = w8_padded_steps(P.A);
-  const size_t lds = static_cast<size_t>(Sp) * 2 * 2 * 64 * 16 + 4 * 32 * 4;
-  BF_REQUIRE(lds <= kMaxLds, "bf_beamform_fused: n_ants=%d too large for the integer wide kernel", P.A);
-  P.nslabs = (P.M + kW8Beams - 1) / kW8Beams;
-  P.xcd_order = P.nslabs > 1 && P.order != BF_FUSED_ORDER_CHANNEL;
-  const long long items = static_cast<long long>(P.B) * P.C;
-  const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
-  BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
-  // Buffer-resource loads (BF_W8_BUFFER=1, signed samples, in-item offsets below 2^31): the contraction alone runs
-  // faster with them (no-coef/no-store 367 vs 394 us), the full kernel slower (609 vs 592 us, interleaved A/B,
-  // profiles/r1_v7_w8_buffer_ab.txt), so the pointer form is the default.
-  const char* bo = diag_env("BF_W8_BUFFER");
-  const bool buf = Signed && static_cast<unsigned long long>(P.A) * P.C * P.T * 4 < (1ull << 31) &&
-                   (bo && bo[0] == '1');
-  if constexpr (Signed) {
-    if (buf) {
-      hipLaunchKernelGGL((beamform_fused_i8_wide_kernel<Signed, Mode, true>), dim3(static_cast<unsigned>(grid)),
-                         dim3(kW8Threads), lds, st, P);
-      BF_LAUNCHED("beamform_fused_i8_wide_kernel");
-    }
-  }
-    hipLaunchKernelGGL((beamform_fused_i8_wide_kernel<Signed, Mode, false>), dim3(static_cast<unsigned>(grid)),
-                       dim3(kW8Threads), lds, st, P);
-  BF_LAUNCHED("beamform_fused_i8_wide_kernel");
-}
-
-#endif  // BF_DIAG
+#ifdef BF_DIAG
+#include "diag/wide_i8_w8.inc"  // the 16-beam slab kernel (diagnostic build only)
+#endif
 
 // ---- 32-beam slabs (the default integer wide kernel) -------------------------------------------------------------
 // The 16-beam kernel above re-reads each item's voltages once per slab (4x at 64 beams) with a prefetch distance of
@@ -877,10 +559,6 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(F
   const int b = grp / gpb, c0 = (grp - b * gpb) * kCh;
   const int nk = min(kCh, Cn - c0);
   const int m0 = slab * kW32Beams;
-#ifdef BF_DIAG
-  // measurement: static priority 1 for the workgroups with blockIdx bit (knob >> 8) set (knob & 1)
-  if ((P.knob & 1) && ((blockIdx.x >> (P.knob >> 8)) & 1)) __builtin_amdgcn_s_setprio(1);
-#endif
   const int Sp = kSp ? kSp : w32_steps(P.A);
   const int T2 = P.T >> 1;
   const int nchunks = (T2 + 15) >> 4;                      // 32-sample chunks
@@ -1419,476 +1097,9 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ---- the halved-image contraction at config 4's shape (the default with a workspace there) ----------------------
-// The table (q14_image_kernel, kLayoutW32H) is the LDS image itself: per (b, c, slab) the (Wc, -Ws) limb fragments of
-// 32 beams x 8 k-steps (32 KiB, half the w32t kernel's image) and the slab's column sums.  A workgroup copies the
-// next channel's image into the other of two LDS buffers by LDS-DMA (global_load_lds_dwordx4, 33 x 1 KiB) as the
-// current channel starts -- no table registers, no expansion, no table latency at the channel barrier -- and every
-// k-step builds two B fragments per pol and sample, [x_re, x_im] for y_re and [x_im, ~x_re] for y_im
-// (w32_frags_im), against the same A fragments: 32 MFMAs per step as before, half the LDS fragment reads.
-//   y_re = sum x_re Wc + x_im (-Ws)                            (+ 128 sum (Wc - Ws) for unsigned samples)
-//   y_im = sum x_im Wc + ~x_re (-Ws) - sum Ws                  (+ 128 sum (Wc + Ws) for unsigned samples)
-// Shape: 8 k-steps (224 < A <= 256), T = 256 (2 passes of 8 straight-line steps per wave, 2-buffer voltage ring),
-// M % 32 == 0, voltage offsets within a workgroup and the beams below 2^31 bytes; 8 channels per workgroup.  The DMA's completion is never waited for explicitly: it is issued before
-// the channel's first refill of the voltage ring, and vmcnt retires in order, so the compiler's own wait for any later
-// voltage load (long before the channel ends) covers it; the LDS reads of the other buffer need no wait at all (the
-// compiler does not see the DMA, so it inserts none).
-constexpr int kW32HChannels = 8;
-constexpr int kW32HItemWords = 8 * 1024 + kW32HSumWords;  // w32h_item_words(8)
-
-// y_im's B fragment from y_re's: [x_re, x_im, ...] -> [x_im, ~x_re, ...] per antenna (one xor + one v_perm per
-// dword; the same for unsigned samples, whose fragments already hold x - 128).
-__device__ __forceinline__ i32x4_t frag_im(const i32x4_t& f) {
-  i32x4_t r;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t n = static_cast<uint32_t>(f[q]) ^ 0x00ff00ffu;
-    r[q] = static_cast<int>(__builtin_amdgcn_perm(n, n, 0x02030001u));
-  }
-  return r;
-}
-
-// The two LDS image buffers as distinct objects: the compiler's alias analysis then knows that an LDS-DMA into one
-// and the ds_reads of the other never overlap, and its own s_waitcnt bookkeeping covers the DMA (it counts it in
-// vmcnt and waits for it only before reading the buffer it writes).  With one array indexed by the channel parity it
-// waited vmcnt(0) before every fragment read; with the DMA hidden in inline asm it over-waited on the voltage ring.
-__shared__ __attribute__((aligned(16))) int4 w32h_img0[kW32HItemWords / 4];
-__shared__ __attribute__((aligned(16))) int4 w32h_img1[kW32HItemWords / 4];
-
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
-
-// Mode (diagnostics only): 16 the y_im MFMAs on y_re's fragment xor a constant (half the frag_im VALU; wrong beams),
-// 128 per-wave s_memtime phase cycles -> P.gain as uint64 [block][wave][4]: waiting for the step's voltages (to the
-// first fragment), the rest of the steps, requantise + stores, the channel barrier.
-template <bool Signed, bool Pow2, int Mode = 0>
-__global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32h_kernel(FusedArgs P) {
-  constexpr int Sp = 8, NP = 2, NB = 2, kCh = kW32HChannels;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 4, tl = lane & 15;
-  const int C = P.C;
-  const int gpb = (C + kCh - 1) / kCh;  // channel groups per batch
-  int slab, grp;
-  if (P.xcd_order) {  // the slabs of one channel group back to back on one XCD: the second re-reads from L2
-    const int x = blockIdx.x & 7, local = blockIdx.x >> 3;
-    slab = local % P.nslabs;
-    grp = (local / P.nslabs) * 8 + x;
-    if (grp >= P.B * gpb) return;
-  } else {
-    slab = blockIdx.x % P.nslabs;
-    grp = blockIdx.x / P.nslabs;
-  }
-  const int b = grp / gpb, c0 = (grp - b * gpb) * kCh;
-  const int nk = min(kCh, C - c0);
-  const int m0 = slab * kW32Beams;
-  const size_t ant_stride = static_cast<size_t>(C) * P.T * 4;
-  const uint32_t hoff = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride);
-  const uint32_t ch_bytes = static_cast<uint32_t>(P.T) * 4;
-  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * C + c0) * static_cast<size_t>(P.T) * 4;
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);  // (tid >> 6 is not provably uniform)
-  // the table as a buffer resource (the host checks its size < 2^31)
-  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(P.table), 0, 0x7fffffff,
-                                                                        0x00020000);
-  const uint32_t titem = static_cast<uint32_t>(((b * C + c0) * P.nslabs + slab) * kW32HItemWords * 4);
-  const uint32_t tch = static_cast<uint32_t>(P.nslabs * kW32HItemWords * 4);  // bytes per channel
-  const uint32_t lvoff = 16u * static_cast<uint32_t>(lane);
-  // half hf of this wave's part of channel kc's item -> image buffer img: 4 of the 32 one-KiB image pieces, and the
-  // wave's quarter of the 1 KiB column-sum block (both halves copy it: the same bytes twice, so they are alike)
-  auto dma_half = [&](int kc, int4* img, int hf) {
-    const uint32_t src = titem + static_cast<uint32_t>(kc) * tch;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int pc = wave_u + 4 * (k + 4 * hf);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void_ptr)(img + 64 * pc), 16, lvoff,
-                                               src + 1024u * static_cast<uint32_t>(pc), 0, 0);
-    }
-    const int cs = 8192 + 64 * wave_u;  // words
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void_ptr)(reinterpret_cast<int*>(img) + cs), 4,
-                                             lvoff >> 2, src + 4u * static_cast<uint32_t>(cs), 0, 0);
-  };
-
-  // the voltage prefetch: step ls of pass lp of channel lk next, across the workgroup's channels
-  const int total = nk * NP * Sp;
-  int issued = 0, ls = 0, lp = 0, lk = 0;
-  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7fffffff,
-                                                                        0x00020000);
-  // T = 256: a wave's sample pairs (wave + 4 pass) * 16 + tl never need the clamp; the lane's part of the offset is
-  // one constant VGPR, the rest (step, pass, channel) goes to the SGPR offset
-  const uint32_t lvo = hoff + 8u * static_cast<uint32_t>(tl);
-  auto issue = [&](u32x2_t (&d)[8]) {
-    const uint32_t sbase = static_cast<uint32_t>(w8_step_base(ls, P.A)) * static_cast<uint32_t>(ant_stride) +
-                           static_cast<uint32_t>(lk) * ch_bytes + static_cast<uint32_t>(wave_u + 4 * lp) * 128u;
-    w32_load_buf<0>(vrs, lvo, sbase, static_cast<uint32_t>(ant_stride), d);
-    ++issued;  // selects, not branches; past the last step it repeats that step
-    const bool adv = issued < total;
-    const bool wrap = ls + 1 == Sp, pwrap = lp + 1 == NP;
-    ls = adv ? (wrap ? 0 : ls + 1) : ls;
-    lp = (adv && wrap) ? (pwrap ? 0 : lp + 1) : lp;
-    lk = (adv && wrap && pwrap) ? lk + 1 : lk;
-  };
-  u32x2_t db[NB][8];
-  dma_half(0, w32h_img0, 0);
-  dma_half(0, w32h_img0, 1);
-#pragma unroll
-  for (int j = 0; j < NB; ++j) issue(db[j]);
-  // every wave's part of channel 0's image landed (all but the 16 voltage loads issued after it) before the barrier
-  __builtin_amdgcn_s_waitcnt(0x4f70);  // vmcnt(16): vmcnt[3:0] = 0, [15:14] = 1
-  lds_barrier();
-
-  const float s32 = P.out_scale * 0x1p-14f;
-  const int M2 = 2 * P.M;
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(P.y, 0, 0x7fffffff, 0x00020000);
-  // the lane's part of a beam-row store offset (sample 2 tl + i of the wave's 32, row piece of lane group h)
-  const uint32_t so_lane = static_cast<uint32_t>(2 * tl * M2 + 16 * (h >> 1) + 32 * (h & 1));
-  unsigned long long st_w = 0, st_m = 0, st_s = 0, st_b = 0, st_t = 0;
-  auto stamp = [&]() -> unsigned long long {
-    if constexpr ((Mode & 128) != 0) return __builtin_amdgcn_s_memtime();
-    return 0ull;
-  };
-  // one channel on image buffer `img` (the next channel's image DMA'd into `nxt`, half in each pass after step 1's
-  // refill; the last channel re-copies itself there, unread)
-  auto channel = [&](int kc, int4* img, int4* nxt) {
-    const int c = c0 + kc;
-    const int knext = min(kc + 1, nk - 1);
-    const int* csums = reinterpret_cast<const int*>(img) + 8192;  // [beam][sum Wc, sum Ws] of the slab
-#pragma unroll 1
-    for (int pass = 0; pass < NP; ++pass) {
-      i32x4_t rh[2][2][2], rl[2][2][2], ih[2][2][2], il[2][2][2];  // [pol][sample i][tile]
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) rh[p][i][t] = rl[p][i][t] = ih[p][i][t] = il[p][i][t] = i32x4_t{0, 0, 0, 0};
-#pragma unroll
-      for (int s = 0; s < Sp; ++s) {
-        const int j = s % NB;  // (Sp * pass is even)
-        i32x4_t f[2][2];
-        const unsigned long long t0 = stamp();
-        w32_frags<Signed>(db[j], f);
-        if constexpr ((Mode & 128) != 0) {  // the fragments exist: the voltage wait is over
-          __builtin_amdgcn_sched_barrier(0);
-          asm volatile("" ::"v"(f[0][0][0]), "v"(f[1][1][3]));
-          const unsigned long long t1 = stamp();
-          st_w += t1 - t0;
-          st_t = t1;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        issue(db[j]);
-        if (s == 1) dma_half(knext, nxt, pass);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int4 x0 = img[((s * 2 + t) * 2 + 0) * 64 + lane];
-          const int4 x1 = img[((s * 2 + t) * 2 + 1) * 64 + lane];
-          const i32x4_t ahi = i32x4_t{x0.x, x0.y, x0.z, x0.w}, alo = i32x4_t{x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-          for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-              // y_im's fragment rebuilt per tile (2 VALU per dword): fewer live registers than keeping all four
-              const i32x4_t fi = (Mode & 16) ? (f[p][i] ^ 0x00ff00ff) : frag_im(f[p][i]);
-              rh[p][i][t] = mfma_i8(ahi, f[p][i], rh[p][i][t]);
-              rl[p][i][t] = mfma_i8(alo, f[p][i], rl[p][i][t]);
-              ih[p][i][t] = mfma_i8(ahi, fi, ih[p][i][t]);
-              il[p][i][t] = mfma_i8(alo, fi, il[p][i][t]);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr ((Mode & 128) != 0) st_m += stamp() - st_t;
-      }
-      const unsigned long long ts0 = stamp();
-      // requantise + store: lane (tl, h) holds beams 16 t + 4 h + r (re and im) of samples 2 tq2 + i; per tile two
-      // dwords [re, im, re, im] (beams 4h, 4h+1 | 4h+2, 4h+3) = bytes [32 t + 8 h, + 8) of the slab's 64-byte row.
-      // One permlane16_swap per dword pair gives lane group h the 16 bytes at 16 (h >> 1) + 32 (h & 1).
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const size_t prow = ((static_cast<size_t>(b) * 2 + p) * C + c) * static_cast<size_t>(P.T);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          uint32_t pk[2][2];  // [tile][dword]
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            // the bias corrections of beams 16 t + 4 h + r from the column sums (sum Wc, sum Ws)
-            const int4 q0 = *reinterpret_cast<const int4*>(csums + 2 * (16 * t + 4 * h));
-            const int4 q1 = *reinterpret_cast<const int4*>(csums + 2 * (16 * t + 4 * h) + 4);
-            const int wc[4] = {q0.x, q0.z, q1.x, q1.z}, ws[4] = {q0.y, q0.w, q1.y, q1.w};
-            uint32_t qr[4], qi[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int cre = Signed ? 0 : 128 * (wc[r] - ws[r]);
-              const int cim = Signed ? -ws[r] : 128 * (wc[r] + ws[r]) - ws[r];
-              qr[r] = requant_bits<Pow2>((rh[p][i][t][r] << 8) + rl[p][i][t][r] + cre, s32);
-              qi[r] = requant_bits<Pow2>((ih[p][i][t][r] << 8) + il[p][i][t][r] + cim, s32);
-            }
-            pk[t][0] = pack_low_bytes(qr[0], qi[0], qr[1], qi[1]);
-            pk[t][1] = pack_low_bytes(qr[2], qi[2], qr[3], qi[3]);
-          }
-          const auto sw0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
-          const auto sw1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-          // through a buffer resource on the beams (32-bit offsets; the host checks the size): the row's base is
-          // wave-uniform (an SGPR soffset), the lane's part one VGPR -- no 64-bit address arithmetic per store
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(u32x4_t, u32x4_t{sw0[0], sw1[0], sw0[1], sw1[1]}), yrs, so_lane,
-              static_cast<uint32_t>((prow + 2 * (wave_u + 4 * pass) * 16 + i) * M2 + 2 * m0), 0);
-        }
-      }
-      if constexpr ((Mode & 128) != 0) st_s += stamp() - ts0;
-    }
-    const unsigned long long tb0 = stamp();
-    // this wave's DMA into `nxt` has landed (the compiler waits for it only before reading `nxt` itself, after the
-    // barrier -- too late for the other waves): everything but the 6 x 8 refills and 4 stores issued after it
-    asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
-    lds_barrier();  // every wave is done with `img`; `nxt` is complete
-    if constexpr ((Mode & 128) != 0) st_b += stamp() - tb0;
-  };
-  for (int kc = 0; kc < nk; kc += 2) {  // (two copies of the body: each reads one buffer, DMAs into the other)
-    channel(kc, w32h_img0, w32h_img1);
-    if (kc + 1 < nk) channel(kc + 1, w32h_img1, w32h_img0);
-  }
-  if constexpr ((Mode & 128) != 0) {
-    unsigned long long* o = reinterpret_cast<unsigned long long*>(const_cast<float*>(P.gain)) +
-                            (static_cast<size_t>(blockIdx.x) * 4 + wave) * 4;
-    if (lane == 0) {
-      o[0] = st_w;
-      o[1] = st_m;
-      o[2] = st_s;
-      o[3] = st_b;
-    }
-  }
-}
-
-// ---- config 4's shape with 64-beam waves (the default with a workspace there) ------------------------------------------
-// The 32-beam kernels run two workgroups per CU, one per slab, so every voltage byte reaches a CU twice (the second
-// slab's read from L2), and the halved-image form above holds 256 VGPRs, which leaves no room to fetch the step's
-// LDS fragments ahead of its MFMAs (steps at ~45 % of the MFMA pipe).  Here a workgroup is 8 waves (two per SIMD)
-// over both slabs of a channel group: a wave owns 16 samples x all 64 beams x 2 pols (128 accumulator registers,
-// as before), each lane loads one 4-byte sample run per antenna (the same load instructions per MFMA as the 32-beam
-// kernels, each byte once per CU), and with ~100 registers to spare the step's 8 A fragments are read at its start,
-// a 4-step voltage ring stays in flight and y_im's fragments are built once per step (24 VALU per 32 MFMAs).  The two
-// slabs' halved images (q14_image_kernel items) are LDS-DMA'd per channel into one of two 66 KiB buffers, slab p's
-// during pass p of the previous channel.  Shape: M = 64, 224 < A <= 256, T = 256 (16 sample chunks: 2 passes of 8).
-constexpr int kW64Threads = 512;
-__shared__ __attribute__((aligned(16))) int4 w64h_img0[2 * kW32HItemWords / 4];
-__shared__ __attribute__((aligned(16))) int4 w64h_img1[2 * kW32HItemWords / 4];
-
-// One step's B fragments [x_re, x_im] per pol from one sample's 8 antenna dwords (unsigned: x - 128).
-template <bool Signed>
-__device__ __forceinline__ void w16_frags(const uint32_t (&d)[8], i32x4_t (&f)[2]) {
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    uint32_t w[4];
-#pragma unroll
-    for (int m2 = 0; m2 < 4; ++m2) {
-      uint32_t a = d[2 * m2], b = d[2 * m2 + 1];
-      if constexpr (!Signed) {
-        a ^= 0x80808080u;
-        b ^= 0x80808080u;
-      }
-      w[m2] = __builtin_amdgcn_perm(b, a, p ? kSelP1 : kSelP0);
-    }
-    f[p] = i32x4_t{static_cast<int>(w[0]), static_cast<int>(w[1]), static_cast<int>(w[2]), static_cast<int>(w[3])};
-  }
-}
-
-// Mode (diagnostics only): 2 no MFMA (a cheap VALU sum instead), 4 no stores, 8 no voltage loads (register-made
-// samples), 32 no image DMA after channel 0.
-template <bool Signed, bool Pow2, int kCh = 16, int NB = 4, int Mode = 0>
-__global__ __launch_bounds__(kW64Threads, 1) void beamform_fused_i8_w64h_kernel(FusedArgs P) {
-  constexpr int Sp = 8, NP = 2;
-  static_assert(Sp % NB == 0, "ring aligned with the passes");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 4, tl = lane & 15;
-  const int C = P.C;
-  const int gpb = (C + kCh - 1) / kCh;  // channel groups per batch
-  const int grp = blockIdx.x;
-  if (grp >= P.B * gpb) return;
-  const int b = grp / gpb, c0 = (grp - b * gpb) * kCh;
-  const int nk = min(kCh, C - c0);
 #ifdef BF_DIAG
-  if ((P.knob & 2) && wave >= 4) __builtin_amdgcn_s_setprio(1);  // measurement: the second-dispatched half first
+#include "diag/wide_i8_w32h.inc"  // round 4's halved-image kernel (diagnostic build only)
 #endif
-  const size_t ant_stride = static_cast<size_t>(C) * P.T * 4;
-  const uint32_t ch_bytes = static_cast<uint32_t>(P.T) * 4;
-  const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * C + c0) * static_cast<size_t>(P.T) * 4;
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(P.table), 0, 0x7fffffff,
-                                                                        0x00020000);
-  const uint32_t titem = static_cast<uint32_t>((b * C + c0) * 2 * kW32HItemWords * 4);  // (b, c0, slab 0)
-  const uint32_t tch = static_cast<uint32_t>(2 * kW32HItemWords * 4);                   // bytes per channel
-  const uint32_t lvoff = 16u * static_cast<uint32_t>(lane);
-  // slab sl's item of channel kc -> half sl of image buffer img: 4 of its 32 image KiB per wave, and a quarter of
-  // its 1 KiB column-sum block (waves w and w + 4 copy the same quarter)
-  auto dma_slab = [&](int kc, int4* img, int sl) {
-    const uint32_t src = titem + static_cast<uint32_t>(kc) * tch + static_cast<uint32_t>(sl * kW32HItemWords * 4);
-    int4* dst = img + sl * (kW32HItemWords / 4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int pc = wave_u + 8 * k;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void_ptr)(dst + 64 * pc), 16, lvoff,
-                                               src + 1024u * static_cast<uint32_t>(pc), 0, 0);
-    }
-    const int cs = 8192 + 64 * (wave_u & 3);  // words
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void_ptr)(reinterpret_cast<int*>(dst) + cs), 4, lvoff >> 2,
-                                             src + 4u * static_cast<uint32_t>(cs), 0, 0);
-  };
-
-  const int total = nk * NP * Sp;
-  int issued = 0, ls = 0, lp = 0, lk = 0;
-  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7fffffff,
-                                                                        0x00020000);
-  // lane (tl, h): sample tl of the wave's 16, antennas 8 h + q of the step; the rest of the offset is uniform
-  const uint32_t lvo = static_cast<uint32_t>(8 * h) * static_cast<uint32_t>(ant_stride) + 4u * static_cast<uint32_t>(tl);
-  auto issue = [&](uint32_t (&d)[8]) {
-    const uint32_t sbase = static_cast<uint32_t>(w8_step_base(ls, P.A)) * static_cast<uint32_t>(ant_stride) +
-                           static_cast<uint32_t>(lk) * ch_bytes + static_cast<uint32_t>(wave_u + 8 * lp) * 64u;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      if constexpr ((Mode & 8) != 0) {
-        d[q] = lvo * 0x01010101u + sbase + q;
-        continue;
-      }
-      d[q] = __builtin_amdgcn_raw_buffer_load_b32(vrs, lvo, sbase + static_cast<uint32_t>(q) * static_cast<uint32_t>(ant_stride), 0);
-    }
-    ++issued;
-    const bool adv = issued < total;
-    const bool wrap = ls + 1 == Sp, pwrap = lp + 1 == NP;
-    ls = adv ? (wrap ? 0 : ls + 1) : ls;
-    lp = (adv && wrap) ? (pwrap ? 0 : lp + 1) : lp;
-    lk = (adv && wrap && pwrap) ? lk + 1 : lk;
-  };
-  uint32_t db[NB][8];
-  dma_slab(0, w64h_img0, 0);
-  dma_slab(0, w64h_img0, 1);
-#pragma unroll
-  for (int j = 0; j < NB; ++j) issue(db[j]);
-  if constexpr (NB == 4) {
-    __builtin_amdgcn_s_waitcnt(0x8f70);  // vmcnt(32): the image DMAs (all but the 32 voltage loads after them)
-  } else {
-    static_assert(NB == 2, "ring depth");
-    __builtin_amdgcn_s_waitcnt(0x4f70);  // vmcnt(16)
-  }
-  lds_barrier();
-
-  const float s32 = P.out_scale * 0x1p-14f;
-  const int M2 = 2 * P.M;  // 128
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(P.y, 0, 0x7fffffff, 0x00020000);
-  const uint32_t so_lane = static_cast<uint32_t>(tl * M2 + 16 * (h >> 1) + 32 * (h & 1));
-  // Mode 64: the next channel's slab through registers instead of LDS-DMA -- 4 x 16-byte loads + 1 dword per lane at
-  // step 1 of a pass, written to LDS at step 5 (the DMA's issue cost measured ~60 us per launch at config 4)
-  u32x4_t tq[4];
-  uint32_t tcs = 0;
-  auto table_load = [&](int kc, int sl) {
-    const uint32_t src = titem + static_cast<uint32_t>(kc) * tch + static_cast<uint32_t>(sl * kW32HItemWords * 4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      tq[k] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                             trs, lvoff, src + 1024u * static_cast<uint32_t>(wave_u + 8 * k), 0));
-    tcs = __builtin_amdgcn_raw_buffer_load_b32(trs, lvoff >> 2, src + 4u * static_cast<uint32_t>(8192 + 64 * (wave_u & 3)), 0);
-  };
-  auto table_store = [&](int4* img, int sl) {
-    int4* dst = img + sl * (kW32HItemWords / 4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) dst[64 * (wave_u + 8 * k) + lane] = __builtin_bit_cast(int4, tq[k]);
-    reinterpret_cast<uint32_t*>(dst)[8192 + 64 * (wave_u & 3) + lane] = tcs;
-  };
-  auto channel = [&](int kc, int4* img, int4* nxt) {
-    const int c = c0 + kc;
-    const int knext = min(kc + 1, nk - 1);
-#pragma unroll 1
-    for (int pass = 0; pass < NP; ++pass) {
-      i32x4_t rh[2][4], rl[2][4], ih[2][4], il[2][4];  // [pol][tile of 16 beams]
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) rh[p][t] = rl[p][t] = ih[p][t] = il[p][t] = i32x4_t{0, 0, 0, 0};
-#pragma unroll
-      for (int s = 0; s < Sp; ++s) {
-        const int j = s % NB;  // (Sp * pass is a multiple of NB)
-        // the step's A fragments first: their LDS latency runs under the fragment VALU and the ring refill
-        i32x4_t ahi[4], alo[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int4* im = img + (t >> 1) * (kW32HItemWords / 4);
-          const int4 x0 = im[((s * 2 + (t & 1)) * 2 + 0) * 64 + lane];
-          const int4 x1 = im[((s * 2 + (t & 1)) * 2 + 1) * 64 + lane];
-          ahi[t] = i32x4_t{x0.x, x0.y, x0.z, x0.w};
-          alo[t] = i32x4_t{x1.x, x1.y, x1.z, x1.w};
-        }
-        i32x4_t f[2], fi[2];
-        w16_frags<Signed>(db[j], f);
-        fi[0] = frag_im(f[0]);
-        fi[1] = frag_im(f[1]);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(db[j]);
-        if constexpr ((Mode & 64) != 0) {
-          if (s == 1) table_load(knext, pass);
-          if (s == 5) table_store(nxt, pass);
-        } else if ((Mode & 32) == 0 && s == 1) {
-          dma_slab(knext, nxt, pass);  // slab `pass` of the next channel
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int p = 0; p < 2; ++p) {
-            if constexpr ((Mode & 2) != 0) {
-              rh[p][t] += ahi[t] + f[p];
-              rl[p][t] += alo[t] ^ fi[p];
-              continue;
-            }
-            rh[p][t] = mfma_i8(ahi[t], f[p], rh[p][t]);
-            rl[p][t] = mfma_i8(alo[t], f[p], rl[p][t]);
-            ih[p][t] = mfma_i8(ahi[t], fi[p], ih[p][t]);
-            il[p][t] = mfma_i8(alo[t], fi[p], il[p][t]);
-          }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // requantise + store: per pol two 16-byte row pieces, one per slab (tiles 2 sl, 2 sl + 1)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const size_t prow = ((static_cast<size_t>(b) * 2 + p) * C + c) * static_cast<size_t>(P.T);
-        const uint32_t srow = static_cast<uint32_t>((prow + 16 * (wave_u + 8 * pass)) * M2);
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-          const int* csums = reinterpret_cast<const int*>(img + sl * (kW32HItemWords / 4)) + 8192;
-          uint32_t pk[2][2];  // [tile of the slab][dword]
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt) {
-            const int t = 2 * sl + tt;
-            const int4 q0 = *reinterpret_cast<const int4*>(csums + 2 * (16 * tt + 4 * h));
-            const int4 q1 = *reinterpret_cast<const int4*>(csums + 2 * (16 * tt + 4 * h) + 4);
-            const int wc[4] = {q0.x, q0.z, q1.x, q1.z}, ws[4] = {q0.y, q0.w, q1.y, q1.w};
-            uint32_t qr[4], qi[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int cre = Signed ? 0 : 128 * (wc[r] - ws[r]);
-              const int cim = Signed ? -ws[r] : 128 * (wc[r] + ws[r]) - ws[r];
-              qr[r] = requant_bits<Pow2>((rh[p][t][r] << 8) + rl[p][t][r] + cre, s32);
-              qi[r] = requant_bits<Pow2>((ih[p][t][r] << 8) + il[p][t][r] + cim, s32);
-            }
-            pk[tt][0] = pack_low_bytes(qr[0], qi[0], qr[1], qi[1]);
-            pk[tt][1] = pack_low_bytes(qr[2], qi[2], qr[3], qi[3]);
-          }
-          const auto sw0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
-          const auto sw1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-          if constexpr ((Mode & 4) != 0) {  // keep the values live, store almost nothing
-            if ((sw0[0] ^ sw1[1]) == 0x12345678u)
-              reinterpret_cast<uint32_t*>(P.y)[tid] = sw0[1] + sw1[0];
-          } else {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, u32x4_t{sw0[0], sw1[0], sw0[1], sw1[1]}),
-                                                   yrs, so_lane, srow + static_cast<uint32_t>(64 * sl), 0);
-          }
-        }
-      }
-    }
-    // this wave's DMA into `nxt` (the last at pass 1 step 1) has landed: all but the 6 x 8 later refills and the 4
-    // stores of pass 1
-    if constexpr ((Mode & 64) == 0) asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
-    lds_barrier();  // every wave is done with `img`; `nxt` is complete
-  };
-  for (int kc = 0; kc < nk; kc += 2) {  // (two copies of the body: each reads one buffer, DMAs into the other)
-    channel(kc, w64h_img0, w64h_img1);
-    if (kc + 1 < nk) channel(kc + 1, w64h_img1, w64h_img0);
-  }
-}
 
 template <bool Signed, int Mode>
 int launch_w32t_contract(FusedArgs P, hipStream_t st);
@@ -1896,31 +1107,6 @@ int launch_w32t_contract(FusedArgs P, hipStream_t st);
 template <bool Signed, int Mode>
 int launch_w32_overlapped(FusedArgs P, int k, hipStream_t st);
 #endif
-
-// The halved-image kernel's shape (beamform_fused_i8_w32h_kernel): 8 k-steps, T = 256, whole 32-beam slabs, every
-// in-workgroup voltage offset below 2^31, a whole launch (no channel chunk).
-bool w32h_fits(const FusedArgs& P) {
-  return w32_steps(P.A) == 8 && P.A > 224 && P.T == 256 && P.M % kW32Beams == 0 && P.c_count == 0 &&
-         static_cast<unsigned long long>(P.A) * P.C * P.T * 4 < (1ull << 31) &&
-         static_cast<unsigned long long>(P.B) * 2 * P.C * P.T * 2 * P.M < (1ull << 31) &&
-         w32_table_bytes(P.B, P.C, P.A, P.M) < (1ull << 31);
-}
-
-// config 4's exact shape for the one-wave-per-SIMD kernel (beamform_fused_i8_w64h_kernel)
-bool w64h_fits(const FusedArgs& P) { return w32h_fits(P) && P.M == 64; }
-
-template <bool Signed, int kCh = 16, int NB = 4, int Mode = 0>
-int launch_w64h_contract(FusedArgs P, hipStream_t st) {
-  const long long grid = static_cast<long long>(P.B) * ((P.C + kCh - 1) / kCh);
-  BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
-  if (scale_is_pow2(P.out_scale * 0x1p-14f))
-    hipLaunchKernelGGL((beamform_fused_i8_w64h_kernel<Signed, true, kCh, NB, Mode>), dim3(static_cast<unsigned>(grid)),
-                       dim3(kW64Threads), 0, st, P);
-  else
-    hipLaunchKernelGGL((beamform_fused_i8_w64h_kernel<Signed, false, kCh, NB, Mode>), dim3(static_cast<unsigned>(grid)),
-                       dim3(kW64Threads), 0, st, P);
-  BF_LAUNCHED("beamform_fused_i8_w64h_kernel");
-}
 
 // The LDS-DMA ring contraction's shape (beamform_fused_i8_w32r_kernel): 8 k-steps, T = 256, whole 32-beam slabs,
 // every in-workgroup voltage offset and every beam offset below 2^31, a whole launch (no channel chunk).
@@ -1945,22 +1131,6 @@ int launch_w32r_contract(FusedArgs P, hipStream_t st) {
   BF_LAUNCHED("beamform_fused_i8_w32r_kernel");
 }
 
-// The halved-image contraction of one launch whose kLayoutW32H table is ready in P.table on `st`.
-template <bool Signed, int Mode = 0>
-int launch_w32h_contract(FusedArgs P, hipStream_t st) {
-  const size_t lds = 0;  // (static: the two image buffers)
-  const long long groups = static_cast<long long>(P.B) * ((P.C + kW32HChannels - 1) / kW32HChannels);
-  const long long grid = P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs;
-  BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
-  if (scale_is_pow2(P.out_scale * 0x1p-14f))
-    hipLaunchKernelGGL((beamform_fused_i8_w32h_kernel<Signed, true, Mode>), dim3(static_cast<unsigned>(grid)),
-                       dim3(kW8Threads), lds, st, P);
-  else
-    hipLaunchKernelGGL((beamform_fused_i8_w32h_kernel<Signed, false, Mode>), dim3(static_cast<unsigned>(grid)),
-                       dim3(kW8Threads), lds, st, P);
-  BF_LAUNCHED("beamform_fused_i8_w32h_kernel");
-}
-
 template <bool Signed, int Mode = 0>
 int launch_w32(FusedArgs P, hipStream_t st) {
   const size_t lds = w32_lds_bytes(P.A);
@@ -1971,8 +1141,9 @@ int launch_w32(FusedArgs P, hipStream_t st) {
   const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
   BF_REQUIRE(grid < (1LL << 31), "bf_beamform_fused: grid too large");
   if (P.table && w32_table_fits(P.A) && P.table_bytes >= w32_table_bytes(P.B, P.C, P.A, P.M)) {
-    // the coefficient table of this launch, written by q14_table_kernel just before on `st`; measurement
-    // (BF_W32_CHUNKS, diagnostic build): generator and contraction alternated over channel chunks
+    // the coefficient table of this launch, written by q14_table_kernel just before on `st`
+#ifdef BF_DIAG
+    // measurement (BF_W32_CHUNKS): generator and contraction alternated over channel chunks
     const char* ck = diag_env("BF_W32_CHUNKS");
     const int nchunks = ck ? std::max(1, atoi(ck)) : 1;
     if (nchunks > 1 && P.B == 1 && P.c_count == 0 && P.delay_channels == 1) {
@@ -1989,7 +1160,6 @@ int launch_w32(FusedArgs P, hipStream_t st) {
       }
       return BF_OK;
     }
-#ifdef BF_DIAG
     // measurement (BF_W32_OVERLAP = k chunks): the generator's chunks on a second stream, each chunk's contraction
     // on the caller's stream after its chunk of the table.  Measured slower than the serial pair (round 4,
     // profiles/r4_s_overlap_ab.txt: 2 / 4 / 8 chunks 494 / 505 / 843 vs 478 us, bitwise equal), so diagnostic only.
@@ -1997,14 +1167,12 @@ int launch_w32(FusedArgs P, hipStream_t st) {
     const int nover = ov ? std::min(16, std::max(1, atoi(ov))) : 1;
     if (nover > 1 && P.B == 1 && P.c_count == 0 && P.delay_channels == 1)
       return launch_w32_overlapped<Signed, Mode>(P, nover, st);
-#endif
-#ifdef BF_DIAG
-    // measurement (BF_W32H=1 / BF_W64H=1): the halved-image generator + the w32h or w64h contraction at config 4's
-    // shape -- bitwise equal to the table kernel, measured no faster (profiles/r4_*)
-    if (Mode == 0 && w32h_fits(P) && (diag_env("BF_W32H") || (diag_env("BF_W64H") && w64h_fits(P)))) {
+    // measurement (BF_W32H=1): the halved-image generator + the w32h contraction at config 4's shape -- bitwise equal
+    // to the table kernel, measured no faster (profiles/r4_*)
+    if (Mode == 0 && w32h_fits(P) && diag_env("BF_W32H")) {
       const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32H, st);
       if (e != BF_OK) return e;
-      return diag_env("BF_W64H") ? launch_w64h_contract<Signed, 16, 2>(P, st) : launch_w32h_contract<Signed>(P, st);
+      return launch_w32h_contract<Signed>(P, st);
     }
 #endif
     const int e = launch_q14_table(P, const_cast<uint32_t*>(P.table), kLayoutW32, st);
@@ -2058,42 +1226,8 @@ int launch_w32t_contract(FusedArgs P, hipStream_t st) {
 }
 
 #ifdef BF_DIAG
-// Generator and contraction overlapped over k channel chunks: fork the caller's stream to the aux stream, generate
-// every chunk's table there (event per chunk), and contract chunk i on the caller's stream once its table is done.
-// The aux stream waits for everything the caller queued before (a previous launch's contraction may still read
-// the workspace), and the caller's stream waits for every chunk, so the call stays stream-ordered for the caller.
-template <bool Signed, int Mode>
-int launch_w32_overlapped(FusedArgs P, int k, hipStream_t st) {
-  AuxStream* ax = aux_stream();
-  if (!ax) return BF_ERR_HIP;
-  const int per = (P.C + k - 1) / k;
-  BF_HIP(hipEventRecord(ax->ev[0], st));
-  BF_HIP(hipStreamWaitEvent(ax->stream, ax->ev[0], 0));
-  auto chunk = [&](int c0) {
-    FusedArgs Q = P;
-    Q.c_count = std::min(per, P.C - c0);
-    Q.raw = P.raw + static_cast<size_t>(c0) * P.T * 4;
-    Q.y = static_cast<int8_t*>(P.y) + static_cast<size_t>(c0) * P.T * 2 * P.M;
-    Q.table = P.table + static_cast<size_t>(c0) * ((P.M + 31) / 32) * 1024 * w32_table_steps(P.A);
-    Q.base_ch = P.base_ch + c0;
-    return Q;
-  };
-  int i = 0;
-  for (int c0 = 0; c0 < P.C; c0 += per, ++i) {
-    FusedArgs Q = chunk(c0);
-    const int e = launch_q14_table(Q, const_cast<uint32_t*>(Q.table), kLayoutW32, ax->stream);
-    if (e != BF_OK) return e;
-    BF_HIP(hipEventRecord(ax->ev[1 + i], ax->stream));
-  }
-  i = 0;
-  for (int c0 = 0; c0 < P.C; c0 += per, ++i) {
-    BF_HIP(hipStreamWaitEvent(st, ax->ev[1 + i], 0));
-    const int e = launch_w32t_contract<Signed, Mode>(chunk(c0), st);
-    if (e != BF_OK) return e;
-  }
-  return BF_OK;
-}
-#endif  // BF_DIAG
+#include "diag/wide_i8_overlap.inc"  // generator / contraction overlap (measured slower)
+#endif
 
 }  // namespace
 
@@ -2114,214 +1248,5 @@ template int launch_i8_w32<true>(FusedArgs, hipStream_t);
 }  // namespace bf
 
 #ifdef BF_DIAG
-// Diagnostics: the integer wide kernel's ablations (tools/diag_fused.py, DIAG_KERNELS=w8).
-// Mode 128 of the 32-beam kernel writes per-wave phase cycles to `stamps` (uint64 [grid][4 waves][4]).
-extern "C" int bf_diag_w32_stamps(const uint8_t* raw, const float* dv, void* y, void* stamps, int B, int C, int T,
-                                  int A, int M, int Ctot, double ts, void* stream) {
-  bf::FusedArgs P{};
-  P.raw = raw;
-  P.dv = reinterpret_cast<const float4*>(dv);
-  P.y = y;
-  P.gain = reinterpret_cast<const float*>(stamps);  // Mode 128: not gains (the Gain instantiation is not used)
-  P.delay_channels = 1;
-  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
-  P.ctot = Ctot;
-  P.ts = ts;
-  P.k = -3.141592653589793 / (Ctot * ts);
-  P.batch_dt = 1e-3;
-  P.out_scale = 1.0f / 64;
-  P.nslabs = (M + 31) / 32;
-  P.xcd_order = P.nslabs > 1;
-  const long long items = static_cast<long long>(B) * C;
-  const long long grid = P.xcd_order ? (items + 7) / 8 * 8 * P.nslabs : items * P.nslabs;
-  hipLaunchKernelGGL((bf::beamform_fused_i8_w32_kernel<true, 128, false>), dim3(static_cast<unsigned>(grid)),
-                     dim3(bf::kW8Threads), bf::w32_lds_bytes(A), bf::as_stream(stream), P);
-  BF_LAUNCHED("beamform_fused_i8_w32_kernel");
-}
-
-// The table-driven 32-beam kernel alone (the table made once, outside the timing): mode = the kernel's Mode bits
-// (1: no table loads / expansion, 2 no MFMA, 4 no stores, 8 no voltage loads); mode -1 = the table generator alone.
-extern "C" int bf_diag_w32_table(int mode, const uint8_t* raw, const float* dv, void* y, void* table, int B, int C,
-                                 int T, int A, int M, int Ctot, double ts, void* stream) {
-  bf::FusedArgs P{};
-  P.raw = raw;
-  P.dv = reinterpret_cast<const float4*>(dv);
-  P.y = y;
-  P.table = static_cast<const uint32_t*>(table);
-  P.table_bytes = bf::w32_table_bytes(B, C, A, M);
-  P.delay_channels = 1;
-  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
-  P.ctot = Ctot;
-  P.ts = ts;
-  P.k = -3.141592653589793 / (Ctot * ts);
-  P.batch_dt = 1e-3;
-  P.out_scale = 1.0f / 64;
-  P.nslabs = (M + 31) / 32;
-  P.xcd_order = P.nslabs > 1;
-  hipStream_t st = bf::as_stream(stream);
-  if (const char* kb = bf::diag_env("BF_KNOB")) P.knob = atoi(kb);  // measurement knobs (bf_fused.hpp)
-  if (mode == -2) return bf::launch_q14_table(P, static_cast<uint32_t*>(table), bf::kLayoutW32H, st);
-  if (mode < 0) return bf::launch_q14_table(P, static_cast<uint32_t*>(table), bf::kLayoutW32, st);
-  if (mode >= 1200 && mode < 1300) {  // the one-wave-per-SIMD contraction alone: kCh 16 / 8, NB 4 / 2
-    switch (mode) {
-      case 1200: return bf::launch_w64h_contract<true, 16, 4>(P, st);
-      case 1201: return bf::launch_w64h_contract<true, 8, 4>(P, st);
-      case 1202: return bf::launch_w64h_contract<true, 16, 2>(P, st);
-      case 1210: return bf::launch_w64h_contract<true, 16, 4, 2>(P, st);
-      case 1211: return bf::launch_w64h_contract<true, 16, 4, 4>(P, st);
-      case 1212: return bf::launch_w64h_contract<true, 16, 4, 8>(P, st);
-      case 1213: return bf::launch_w64h_contract<true, 16, 4, 12>(P, st);
-      case 1214: return bf::launch_w64h_contract<true, 16, 4, 6>(P, st);
-      case 1215: return bf::launch_w64h_contract<true, 16, 4, 32>(P, st);
-      case 1216: return bf::launch_w64h_contract<true, 16, 4, 14>(P, st);
-      case 1220: return bf::launch_w64h_contract<true, 16, 2, 64>(P, st);
-      case 1221: return bf::launch_w64h_contract<true, 16, 4, 64>(P, st);
-      case 1222: return bf::launch_w64h_contract<true, 16, 2, 32>(P, st);
-      default: return BF_ERR_ARG;
-    }
-  }
-  if (mode >= 2000 && mode < 2100) {  // the LDS-DMA ring contraction alone (the kLayoutW32 table); +Mode bits
-    switch (mode - 2000) {
-      case 0: return bf::launch_w32r_contract<0>(P, st);
-      case 4: return bf::launch_w32r_contract<4>(P, st);
-      case 8: return bf::launch_w32r_contract<8>(P, st);
-      case 12: return bf::launch_w32r_contract<12>(P, st);
-      case 16: return bf::launch_w32r_contract<16>(P, st);
-      case 24: return bf::launch_w32r_contract<24>(P, st);
-      default: return BF_ERR_ARG;
-    }
-  }
-  if (mode >= 960 && mode < 1200) {  // the halved-image contraction alone (a kLayoutW32H table in `table`); +Mode bits
-    P.nslabs = (M + 31) / 32;
-    P.xcd_order = P.nslabs > 1;
-    switch (mode - 960) {
-      case 0: return bf::launch_w32h_contract<true, 0>(P, st);
-      case 16: return bf::launch_w32h_contract<true, 16>(P, st);
-      default: return BF_ERR_ARG;  // (Mode 128 needs a stamps buffer: bf_diag_w32h_stamps)
-    }
-  }
-  const long long groups = static_cast<long long>(B) * ((C + bf::kW32TChannels - 1) / bf::kW32TChannels);
-  const unsigned grid = static_cast<unsigned>(P.xcd_order ? (groups + 7) / 8 * 8 * P.nslabs : groups * P.nslabs);
-  const size_t lds = bf::w32_lds_bytes(A);
-  auto grid_for = [&](int ch) {  // channels per workgroup other than kW32TChannels (measurement)
-    const long long g = static_cast<long long>(B) * ((C + ch - 1) / ch);
-    return static_cast<unsigned>(P.xcd_order ? (g + 7) / 8 * 8 * P.nslabs : g * P.nslabs);
-  };
-#define BF_W32T(m) \
-  case m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 100 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 300 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 400 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 4>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 200 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 220 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 2>), dim3(grid_for(2)), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 240 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 260 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 16>), dim3(grid_for(16)), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 280 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, true, 8, 2, 2, 8>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, true, 8, 2, 3>), dim3(grid), dim3(bf::kW8Threads), lds, st, P); break
-#define BF_W32TB(m) \
-  case 900 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8, true, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 920 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 3, 8, true, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break; \
-  case 940 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8, false, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break
-  switch (mode) {
-    BF_W32T(0); BF_W32T(1); BF_W32T(4); BF_W32T(8); BF_W32T(9); BF_W32T(12);
-    BF_W32TB(0); BF_W32TB(1); BF_W32TB(4); BF_W32TB(8); BF_W32TB(9); BF_W32TB(12); BF_W32TB(16); BF_W32TB(17);
-#define BF_W32TP(m) \
-  case 1500 + m: hipLaunchKernelGGL((bf::beamform_fused_i8_w32t_kernel<true, m, false, 8, 2, 2, 8, true, true>), dim3(grid_for(8)), dim3(bf::kW8Threads), lds, st, P); break
-    BF_W32TP(32); BF_W32TP(33); BF_W32TP(36); BF_W32TP(40); BF_W32TP(64); BF_W32TP(128); BF_W32TP(192);
-    BF_W32TP(256); BF_W32TP(257); BF_W32TP(260);
-#undef BF_W32TP
-    default: return BF_ERR_ARG;
-  }
-#undef BF_W32TB
-#undef BF_W32T
-  BF_LAUNCHED("beamform_fused_i8_w32t_kernel");
-}
-
-// The halved-image contraction with per-wave phase stamps (Mode 128): uint64 [grid][4 waves][4] -> stamps.
-extern "C" int bf_diag_w32h_stamps(const uint8_t* raw, const void* table, void* y, void* stamps, int B, int C, int T,
-                                   int A, int M, void* stream) {
-  bf::FusedArgs P{};
-  P.raw = raw;
-  P.y = y;
-  P.table = static_cast<const uint32_t*>(table);
-  P.gain = static_cast<const float*>(stamps);
-  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
-  P.out_scale = 1.0f / 64;
-  P.nslabs = (M + 31) / 32;
-  P.xcd_order = P.nslabs > 1;
-  return bf::launch_w32h_contract<true, 128>(P, bf::as_stream(stream));
-}
-
-// The whole table-driven launch (generator + contraction, as bf_beamform_fused_ws runs it); BF_W32_CHUNKS splits it
-// into alternating per-chunk generator / contraction launches.
-extern "C" int bf_diag_w32_launch(const uint8_t* raw, const float* dv, void* y, void* table, int B, int C, int T,
-                                  int A, int M, int Ctot, double ts, void* stream) {
-  bf::FusedArgs P{};
-  P.raw = raw;
-  P.dv = reinterpret_cast<const float4*>(dv);
-  P.y = y;
-  P.table = static_cast<const uint32_t*>(table);
-  P.table_bytes = bf::w32_table_bytes(B, C, A, M);
-  P.delay_channels = 1;
-  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
-  P.ctot = Ctot;
-  P.ts = ts;
-  P.k = -3.141592653589793 / (Ctot * ts);
-  P.batch_dt = 1e-3;
-  P.out_scale = 1.0f / 64;
-  return bf::launch_w32<true, 0>(P, bf::as_stream(stream));
-}
-
-extern "C" int bf_diag_w8(int mode, const uint8_t* raw, const float* dv, void* y, int B, int C, int T, int A, int M,
-                          int Ctot, double ts, void* stream) {
-  bf::FusedArgs P{};
-  P.raw = raw;
-  P.dv = reinterpret_cast<const float4*>(dv);
-  P.y = y;
-  P.delay_channels = 1;
-  P.B = B, P.C = C, P.T = T, P.A = A, P.M = M;
-  P.ctot = Ctot;
-  P.ts = ts;
-  P.k = -3.141592653589793 / (Ctot * ts);
-  P.batch_dt = 1e-3;
-  P.out_scale = 1.0f / 64;
-  hipStream_t st = bf::as_stream(stream);
-  switch (mode) {
-    case 0: return bf::launch_w8<true, 0>(P, st);
-    case 1: return bf::launch_w8<true, 1>(P, st);
-    case 2: return bf::launch_w8<true, 2>(P, st);
-    case 4: return bf::launch_w8<true, 4>(P, st);
-    case 8: return bf::launch_w8<true, 8>(P, st);
-    case 5: return bf::launch_w8<true, 5>(P, st);
-    case 3: return bf::launch_w8<true, 3>(P, st);
-    case 9: return bf::launch_w8<true, 9>(P, st);
-    case 13: return bf::launch_w8<true, 13>(P, st);
-    case 16 + 3: return bf::launch_w8<true, 16 + 3>(P, st);
-    case 32 + 3: return bf::launch_w8<true, 32 + 3>(P, st);
-    case 48 + 3: return bf::launch_w8<true, 48 + 3>(P, st);
-    case 32: return bf::launch_w8<true, 32>(P, st);
-    case 16 + 1: return bf::launch_w8<true, 16 + 1>(P, st);
-    case 64 + 3: return bf::launch_w8<true, 64 + 3>(P, st);
-    case 64 + 16 + 3: return bf::launch_w8<true, 64 + 16 + 3>(P, st);
-    case 256 + 3: return bf::launch_w8<true, 256 + 3>(P, st);
-    case 256 + 16 + 3: return bf::launch_w8<true, 256 + 16 + 3>(P, st);
-    case 256: return bf::launch_w8<true, 256>(P, st);
-    case 512: return bf::launch_w8<true, 512>(P, st);
-    case 128: return bf::launch_w8<true, 128>(P, st);  // exact phasors only (no fast attempt)
-    // 32-beam slabs: 1000 + the kernel's Mode bits
-    case 1000: return bf::launch_w32<true, 0>(P, st);
-    case 1001: return bf::launch_w32<true, 1>(P, st);
-    case 1002: return bf::launch_w32<true, 2>(P, st);
-    case 1003: return bf::launch_w32<true, 3>(P, st);
-    case 1004: return bf::launch_w32<true, 4>(P, st);
-    case 1008: return bf::launch_w32<true, 8>(P, st);
-    case 1009: return bf::launch_w32<true, 9>(P, st);
-    case 1013: return bf::launch_w32<true, 13>(P, st);
-    case 1016: return bf::launch_w32<true, 16>(P, st);
-    case 1017: return bf::launch_w32<true, 17>(P, st);
-    case 1064: return bf::launch_w32<true, 64>(P, st);    // model loads, no phasor math
-    case 1256: return bf::launch_w32<true, 256>(P, st);   // phasor math, no model loads
-    default: return BF_ERR_ARG;
-  }
-}
+#include "diag/wide_i8_entries.inc"
 #endif

@@ -38,7 +38,7 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "bf_fused.hpp"
+#include "../bf_fused.hpp"
 
 #ifdef BF_DIAG
 namespace bf {

@@ -1,11 +1,13 @@
 #!/bin/bash
-# GPU box, round 5: the LDS-DMA ring contraction (w32r) -- parity on the config-4 tests, then the same-process A/B
-# against the table kernel (w32t) on one kLayoutW32 table.  Usage: bash tools/gpu_r5_w32r.sh <tag>
+# GPU box, round 5: the LDS-DMA ring contraction (w32r) -- bitwise against w32t (3 runs), parity on the config-4
+# tests, then the same-process A/B against the table kernel (w32t) on one kLayoutW32 table.
 set -o pipefail
 TAG=${1:-r5_w}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+timeout -k 10 200 python -u tools/diag_w32r.py 3 2000 > $OUT/w32r_vs_w32t.txt 2>&1 || { echo "diag_w32r failed"; tail -20 $OUT/w32r_vs_w32t.txt; exit 1; }
+cat $OUT/w32r_vs_w32t.txt | cut -c1-200
 timeout -k 10 400 python -u -m pytest tests/test_gpu_fullsize.py tests/test_gpu_q14table.py -m gpu -x -v --timeout 120 \
   --timeout-method thread -p no:cacheprovider > $OUT/pytest_cfg4.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_cfg4.log; exit 1; }
 tail -2 $OUT/pytest_cfg4.log
