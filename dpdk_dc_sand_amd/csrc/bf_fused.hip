@@ -295,7 +295,7 @@ __device__ __forceinline__ void store_pol(const FusedArgs& P, int b, int c, int 
 }
 
 // int8 beams requantised from the float accumulators of a full slab, stored as whole rows (defined below).
-template <int NTS>
+template <int NTS, bool Pow2>
 __device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, int tau0, int tq, int h, int lane,
                                      int wave, bool tv, const f32x4 (&acc)[4][NTS]);
 
@@ -304,7 +304,9 @@ __device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, in
 // Issue order delay model -> voltages (16 x 16 B per lane, all in flight) -> coefficient math under them ->
 // barrier -> per pol: MFMA contraction + stores.  Memory/compute overlap comes from the 3+ workgroups a CU holds
 // at this register footprint (the hardware interleaves their phases).
-template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0, int Occ = 1>
+// Pow2 (int8 beams): out_scale is a power of two, so RN(y * s) is exact and the requantisation's multiply and magic
+// add are one exact FMA (as requant_bits<true>).
+template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0, int Occ = 1, bool Pow2 = false>
 __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_item_kernel(FusedArgs P) {
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_item_kernel(Fuse
       if (sum == 1234.5f) reinterpret_cast<float*>(P.y)[tid] = sum;
     } else {
       if constexpr (OutI8 && Full) {
-        store_f32acc_i8_rows<NTS>(P, b, c, p, tau0, tq, h, lane, wave, tv, acc);
+        store_f32acc_i8_rows<NTS, Pow2>(P, b, c, p, tau0, tq, h, lane, wave, tv, acc);
       } else if constexpr (!OutI8 && Full && NTS == 2 && (Mode & kLdsStoreF32) != 0) {
         // M2 == 32 (launcher): the wave's rows 64 w .. 64 w + 63 of (b, p, c) are one contiguous 8 KiB run
         float* stg = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + static_cast<size_t>(P.S) * NTS * 2 * 64 * 16) +
@@ -826,7 +828,7 @@ __device__ __forceinline__ void i8_store_block(const uint32_t (&pk)[NTS][4], int
 // pack, the 4x4 row transpose, then whole-row stores -- 1 KiB ds_bpermute blocks when the slab is the whole row --
 // instead of one 4-byte store per (sample, tile) (the int8 item kernel's store path, 4x fewer, wider stores).
 // Every lane of the wave must be here (permlane / bpermute); `tv` guards only the stores.
-template <int NTS>
+template <int NTS, bool Pow2>
 __device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, int tau0, int tq, int h, int lane,
                                      int wave, bool tv, const f32x4 (&acc)[4][NTS]) {
   constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
@@ -841,7 +843,9 @@ __device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, in
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v;
-        {
+        if constexpr (Pow2) {
+          v = __builtin_fmaf(acc[i][tau][r], s, kMagic);  // y * s exact: the one FMA is the two roundings
+        } else {
 #pragma clang fp contract(off)  // RN(y * s), then the magic add: two roundings (see requant_bits)
           v = acc[i][tau][r] * s + kMagic;
         }
@@ -1184,8 +1188,8 @@ int launch_i8(FusedArgs P, hipStream_t st) {
   BF_LAUNCHED("beamform_fused_i8_kernel");
 }
 
-template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0, int Occ = 1>
-int launch_item(FusedArgs P, hipStream_t st) {
+template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode, int Occ, bool Pow2>
+int launch_item_k(FusedArgs P, hipStream_t st) {
   P.nslabs = (P.NT + NTS - 1) / NTS;
   P.xcd_order = item_xcd_order(P);
   if constexpr ((Mode & kLdsStoreF32) != 0)
@@ -1193,9 +1197,19 @@ int launch_item(FusedArgs P, hipStream_t st) {
   const size_t lds = coef_lds_bytes(P.S, NTS) + ((Mode & kLdsStoreF32) ? kF32StageBytes : 0);
   const long long n_items = static_cast<long long>(P.nslabs) * P.B * P.C;
   BF_REQUIRE(n_items < (1LL << 31), "bf_beamform_fused: too many (batch, channel) items");
-  hipLaunchKernelGGL((beamform_fused_item_kernel<Signed, OutI8, NTS, Exact, Full, Mode, Occ>),
+  hipLaunchKernelGGL((beamform_fused_item_kernel<Signed, OutI8, NTS, Exact, Full, Mode, Occ, Pow2>),
                      dim3(static_cast<unsigned>(n_items)), dim3(kThreads), lds, st, P);
   BF_LAUNCHED("beamform_fused_item_kernel");
+}
+
+template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0, int Occ = 1>
+int launch_item(FusedArgs P, hipStream_t st) {
+  if constexpr (OutI8) {
+    // a power-of-two scale: the float path's requantisation as one exact FMA (its round-4 two-rounding form had
+    // cost cfg3 int8-via-f32 ~3 %, BENCH_r03 460.8 -> BENCH_r04 476.3 us; A/B in DESIGN §5)
+    if (scale_is_pow2(P.out_scale)) return launch_item_k<Signed, OutI8, NTS, Exact, Full, Mode, Occ, true>(P, st);
+  }
+  return launch_item_k<Signed, OutI8, NTS, Exact, Full, Mode, Occ, false>(P, st);
 }
 
 template <bool Signed, bool OutI8, int NTS, bool Exact>

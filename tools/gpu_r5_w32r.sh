@@ -14,4 +14,11 @@ tail -2 $OUT/pytest_cfg4.log
 DIAG_KERNELS=w32t W32T_MODES=${MODES:-900,2000,2004,2008,2012,2016,2024,908,901,904} DIAG_ROUNDS=5 timeout -k 10 300 \
   python -u tools/diag_fused.py 1 4096 256 256 64 > $OUT/w32r_ab.txt 2>&1 || { echo "diag failed"; tail -20 $OUT/w32r_ab.txt; exit 1; }
 cat $OUT/w32r_ab.txt
+
+# the int8-via-f32 drift: round-3 tree, round-4 tree and this tree in one process
+for fl in 0xb 0x3 0x1; do
+  timeout -k 10 240 python -u tools/ab_libs.py cfg3 $fl 0.015625 r5=dpdk_dc_sand_amd/libbf.so \
+    r4=build/ab_r4/dpdk_dc_sand_amd/libbf.so r3=build/ab_r3/dpdk_dc_sand_amd/libbf.so >> $OUT/ab_rounds.txt 2>&1 || { echo "ab failed"; tail -20 $OUT/ab_rounds.txt; exit 1; }
+done
+cat $OUT/ab_rounds.txt
 echo "run $TAG ok"
