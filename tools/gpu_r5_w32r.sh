@@ -18,7 +18,7 @@ cat $OUT/w32r_ab.txt
 # the int8-via-f32 drift: round-3 tree, round-4 tree and this tree in one process
 for fl in 0xb 0x3 0x1; do
   timeout -k 10 240 python -u tools/ab_libs.py cfg3 $fl 0.015625 r5=dpdk_dc_sand_amd/libbf.so \
-    r4=build/ab_r4/dpdk_dc_sand_amd/libbf.so r3=build/ab_r3/dpdk_dc_sand_amd/libbf.so >> $OUT/ab_rounds.txt 2>&1 || { echo "ab failed"; tail -20 $OUT/ab_rounds.txt; exit 1; }
+    r4=build/libbf_r4.so r3=build/libbf_r3.so >> $OUT/ab_rounds.txt 2>&1 || { echo "ab failed"; tail -20 $OUT/ab_rounds.txt; exit 1; }
 done
 cat $OUT/ab_rounds.txt
 echo "run $TAG ok"
