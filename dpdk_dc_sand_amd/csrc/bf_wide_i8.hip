@@ -864,7 +864,8 @@ __device__ __forceinline__ i32x4_t w32r_frag_im(const i32x4_t& f) {
   return r;
 }
 
-// Mode (diagnostics only): 4 no stores, 8 no voltage DMA (the slots' stale bytes), 16 no table loads / expansion.
+// Mode (diagnostics only): 4 no stores, 8 no voltage DMA (the slots' stale bytes), 16 no table loads / expansion,
+// 32 the step's four DMA pieces spread over its MFMAs (one per 8).
 template <bool Pow2, int Mode = 0>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(FusedArgs P) {
   constexpr int Sp = 8, NP = 2, kCh = kW32RChannels;
@@ -899,23 +900,31 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
   // the voltage ring: step ls of pass lp of channel lk is DMA'd next (past the last step it repeats that step)
   const int total = nk * NP * Sp;
   int issued = 0, ls = 0, lp = 0, lk = 0;
-  auto dma = [&](int4* slot) {
+  // the step's uniform source offset, one 1 KiB piece of its DMA, and the ring's advance (selects, not branches)
+  auto dma_sb = [&]() {
     // (readfirstlane: a loop-carried part of it landed in a VGPR, and the DMA's soffset then became a waterfall loop)
-    const uint32_t sb = __builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(w8_step_base(ls, P.A)) * ant_stride + static_cast<uint32_t>(lk) * ch_bytes +
-        static_cast<uint32_t>(wave + 4 * lp) * 128u);
-    if constexpr ((Mode & 8) == 0) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lds_void_ptr)(slot + 64 * k), 16, dma_voff,
-                                                 sb + 2u * static_cast<uint32_t>(k) * ant_stride, 0, 0);
-    }
+    return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(w8_step_base(ls, P.A)) * ant_stride +
+                                          static_cast<uint32_t>(lk) * ch_bytes +
+                                          static_cast<uint32_t>(wave + 4 * lp) * 128u);
+  };
+  auto dma_piece = [&](int4* slot, int k, uint32_t sb) {
+    if constexpr ((Mode & 8) == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lds_void_ptr)(slot + 64 * k), 16, dma_voff,
+                                               sb + 2u * static_cast<uint32_t>(k) * ant_stride, 0, 0);
+  };
+  auto advance = [&]() {
     ++issued;
     const bool adv = issued < total;
     const bool wrap = ls + 1 == Sp, pwrap = lp + 1 == NP;
     ls = adv ? (wrap ? 0 : ls + 1) : ls;
     lp = (adv && wrap) ? (pwrap ? 0 : lp + 1) : lp;
     lk = (adv && wrap && pwrap) ? lk + 1 : lk;
+  };
+  auto dma = [&](int4* slot) {
+    const uint32_t sb = dma_sb();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dma_piece(slot, k, sb);
+    advance();
   };
   // this lane's 8 antenna rows x its sample pair from the wave's slot: the table kernel's register layout
   auto read_slot = [&](const int4* slot, u32x2_t (&d)[8]) {
@@ -998,14 +1007,23 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
         // nothing else orders a ds_read before a later LDS-DMA write to the same bytes (WAR)
         asm volatile("" ::"v"(f[0][0]), "v"(f[0][1]), "v"(f[1][0]), "v"(f[1][1]) : "memory");
         __builtin_amdgcn_sched_barrier(0);
-        dma(slot);
+        const uint32_t sb = dma_sb();
+        if constexpr ((Mode & 32) == 0) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) dma_piece(slot, k, sb);
+        }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int4 x0 = w32r_img[((s * 2 + t) * 2 + 0) * 64 + lane];
           const int4 x1 = w32r_img[((s * 2 + t) * 2 + 1) * 64 + lane];
           const i32x4_t ahi = i32x4_t{x0.x, x0.y, x0.z, x0.w}, alo = i32x4_t{x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-          for (int p = 0; p < 2; ++p)
+          for (int p = 0; p < 2; ++p) {
+            if constexpr ((Mode & 32) != 0) {  // one DMA piece per 8 MFMAs instead of a burst of 4
+              __builtin_amdgcn_sched_barrier(0);
+              dma_piece(slot, 2 * t + p, sb);
+              __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
               rh[p][i][t] = mfma_i8(ahi, f[p][i], rh[p][i][t]);
@@ -1013,7 +1031,9 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
               ih[p][i][t] = mfma_i8(ahi, fi[p][i], ih[p][i][t]);
               il[p][i][t] = mfma_i8(alo, fi[p][i], il[p][i][t]);
             }
+          }
         }
+        advance();
         __builtin_amdgcn_sched_barrier(0);
       }
       // the next channel's table, requested after the last pass's MFMAs (its latency under the stores and barrier)
