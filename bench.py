@@ -568,16 +568,20 @@ def mfma_split(sec, ent):
     m["generator_share_of_step"] = round(1.0 - contraction_us / total_us, 4)
 
 
-def kernel_name(wl, out_int8, int8_contract="q14", coeff_table="on"):
+def kernel_name(wl, out_int8, int8_contract="q14", coeff_table="on", signed=True):
     """The launch's dominant kernel (bf_fused.hip dispatch): item kernels for A <= 64 and T <= 256, else the wide
-    kernels; the int8 32-beam path with a coefficient table (A <= 256) is the table-driven contraction, after its
-    generator (q14_table_kernel, reported per step beside it)."""
+    kernels; the int8 32-beam path with a coefficient table (A <= 256) is a table-driven contraction after its
+    generator (q14_table_kernel, reported per step beside it): at config 4's shape with int8 samples the LDS-DMA
+    ring kernel (w32r: 224 < A <= 256, T = 256, M % 32 == 0), else the register-ring kernel (w32t)."""
     integer = out_int8 and int8_contract == "q14"
     if wl["A"] <= 64 and wl["T"] <= 256:
         return "beamform_fused_i8_item_kernel" if integer else "beamform_fused_item_kernel"
     if integer:
-        return "beamform_fused_i8_w32t_kernel" if coeff_table == "on" and wl["A"] <= 256 else \
-            "beamform_fused_i8_w32_kernel"
+        if coeff_table != "on" or wl["A"] > 256:
+            return "beamform_fused_i8_w32_kernel"
+        if signed and 224 < wl["A"] <= 256 and wl["T"] == 256 and wl["M"] % 32 == 0:
+            return "beamform_fused_i8_w32r_kernel"
+        return "beamform_fused_i8_w32t_kernel"
     return "beamform_fused_wide_kernel"
 
 
@@ -590,7 +594,7 @@ def secondary(args, dist, workload, out_int8, int8_contract="q14"):
     out = {"workload": workload + ": " + wl["desc"],
            "output": ("int8" + ("" if int8_contract == "q14" else " (requantised from float32 beams)"))
            if out_int8 else "float32",
-           "kernel": kernel_name(wl, out_int8, int8_contract, args.coeff_table),
+           "kernel": kernel_name(wl, out_int8, int8_contract, args.coeff_table, not args.unsigned),
            "value": round(r["samples_per_step"] * args.steps * dist.world / r["t_max"] / 1e9, 2),
            "unit": "Gsamples/s", "n_gpus": dist.world,
            "roofline_frac": round(r["alg_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
@@ -657,7 +661,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "read_frac": round(r["read_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
-                     "kernel": kernel_name(wl, args.out_int8, args.int8_contract, args.coeff_table),
+                     "kernel": kernel_name(wl, args.out_int8, args.int8_contract, args.coeff_table,
+                                           not args.unsigned),
                      "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"],
                      "read_bytes_per_launch": r["read_bytes"]},
         "mfma": mfma_util(wl, args.out_int8, args.int8_contract, r["kernel_s"]),

@@ -32,11 +32,17 @@ def test_realtime_factor_against_meerkat_ingest():
     ("cfg3", True, "f32", "on", "beamform_fused_item_kernel"),
     ("cfg3", False, "q14", "on", "beamform_fused_item_kernel"),
     ("cfg2", True, "q14", "on", "beamform_fused_i8_item_kernel"),
-    ("cfg4", True, "q14", "on", "beamform_fused_i8_w32t_kernel"),
+    ("cfg4", True, "q14", "on", "beamform_fused_i8_w32r_kernel"),
     ("cfg4", True, "q14", "off", "beamform_fused_i8_w32_kernel"),
     ("cfg4", False, "q14", "on", "beamform_fused_wide_kernel")])
 def test_roofline_kernel_per_workload(workload, out_int8, contract, table, expected):
     assert bench.kernel_name(bench.WORKLOADS[workload], out_int8, contract, table) == expected
+
+
+def test_roofline_kernel_unsigned_config4():
+    # uint8 samples keep the register-ring table kernel (the DMA ring kernel is int8-only)
+    assert bench.kernel_name(bench.WORKLOADS["cfg4"], True, "q14", "on", signed=False) == \
+        "beamform_fused_i8_w32t_kernel"
 
 
 def test_short_kernel_names():

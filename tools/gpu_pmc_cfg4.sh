@@ -4,6 +4,6 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc}
 mkdir -p "$OUT"
-PMC_KERNEL=beamform_fused_i8_w32t timeout -k 10 600 python -u tools/pmc_profile.py "$OUT/w32t" -- --workload cfg4 > "$OUT/w32t_pmc.txt" 2>&1 && \
+PMC_KERNEL=beamform_fused_i8_w32r timeout -k 10 600 python -u tools/pmc_profile.py "$OUT/w32r" -- --workload cfg4 > "$OUT/w32r_pmc.txt" 2>&1 && \
 PMC_KERNEL=q14_table timeout -k 10 600 python -u tools/pmc_profile.py "$OUT/gen" -- --workload cfg4 > "$OUT/gen_pmc.txt" 2>&1 && \
 PMC_KERNEL=beamform_fused_wide timeout -k 10 600 python -u tools/pmc_profile.py "$OUT/wide" -- --workload cfg4 --output f32 > "$OUT/wide_pmc.txt" 2>&1
