@@ -865,7 +865,8 @@ __device__ __forceinline__ i32x4_t w32r_frag_im(const i32x4_t& f) {
 }
 
 // Mode (diagnostics only): 4 no stores, 8 no voltage DMA (the slots' stale bytes), 16 no table loads / expansion,
-// 32 the step's four DMA pieces issued as one burst before its MFMAs (the product spreads them, one per 8 MFMAs).
+// 32 the step's four DMA pieces issued as one burst before its MFMAs (the product spreads them, one per 8 MFMAs),
+// 64 a pass's four beam stores back to back after its requantisation.
 template <bool Pow2, int Mode = 0>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(FusedArgs P) {
   constexpr int Sp = 8, NP = 2, kCh = kW32RChannels;
@@ -1072,6 +1073,8 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
             for (int t = 0; t < 2; ++t) sum += rh[p][i][t][0] ^ rl[p][i][t][1] ^ ih[p][i][t][2] ^ il[p][i][t][3] ^ bias[t][p];
         if (sum == 0x12345678) reinterpret_cast<int*>(P.y)[tid] = sum;
       } else {
+        u32x4_t sd[2][2];  // [pol][sample i]: the 16 store bytes of this lane
+        uint32_t soff[2][2];
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           const uint32_t prow = static_cast<uint32_t>(((b * 2 + p) * C + c) * P.T);
@@ -1091,18 +1094,29 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
             }
             const auto sw0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
             const auto sw1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                __builtin_bit_cast(u32x4_t, u32x4_t{sw0[0], sw1[0], sw0[1], sw1[1]}), yrs, so_lane,
-                (prow + static_cast<uint32_t>(2 * (wave + 4 * pass) * 16 + i)) * static_cast<uint32_t>(M2) +
-                    static_cast<uint32_t>(2 * m0),
-                0);
-            // Two wait states before any VALU may rewrite the store's data VGPRs: hipcc scheduled a write of its 4th
-            // data register right behind this store, and that dword of lanes 12-15 of every row went out wrong
-            // (~1e-5 of the bytes, run to run; tools/diag_w32r.py, tools/store_hazard_check.py).
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_nop 1");
-            __builtin_amdgcn_sched_barrier(0);
+            sd[p][i] = u32x4_t{sw0[0], sw1[0], sw0[1], sw1[1]};
+            soff[p][i] = (prow + static_cast<uint32_t>(2 * (wave + 4 * pass) * 16 + i)) * static_cast<uint32_t>(M2) +
+                         static_cast<uint32_t>(2 * m0);
+            if constexpr ((Mode & 64) == 0) {
+              __builtin_amdgcn_raw_buffer_store_b128(sd[p][i], yrs, so_lane, soff[p][i], 0);
+              // Two wait states before any VALU may rewrite the store's data VGPRs: hipcc scheduled a write of its
+              // 4th data register right behind this store, and that dword of lanes 12-15 of every row went out
+              // wrong (~1e-5 of the bytes, run to run; tools/diag_w32r.py, tools/store_hazard_check.py).
+              __builtin_amdgcn_sched_barrier(0);
+              asm volatile("s_nop 1");
+              __builtin_amdgcn_sched_barrier(0);
+            }
           }
+        }
+        if constexpr ((Mode & 64) != 0) {  // (diagnostics: the pass's four stores back to back, one guard)
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_buffer_store_b128(sd[p][i], yrs, so_lane, soff[p][i], 0);
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_nop 1");
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
