@@ -154,7 +154,9 @@ __device__ __forceinline__ void make_coefs(_Float16* lh, const CoefPrefetch<NTS>
       if constexpr (Exact) {
         steering_coeff(cp.dv[j], ch, make_phase(P.ctot, P.ts), dt, &re, &im);
       } else {
-        steering_coeff_fast(cp.dv[j], chc, P.k, dt, &re, &im);
+        // hardware v_sin / v_cos on float64-reduced revolutions (<= 3.2 x 2^-24 from the float64 phasor), as the
+        // wide kernel since round 4: fewer VALU than the float32 polynomials of steering_coeff_fast
+        steering_coeff_hw(cp.dv[j], chc, P.k, dt, &re, &im);
       }
       if (P.gain) apply_gain(cp.g[j], &re, &im);
     }
@@ -183,7 +185,7 @@ __device__ __forceinline__ void gen_coefs(_Float16* lh, const FusedArgs& P, int 
       if constexpr (Exact) {
         steering_coeff(d, ch, make_phase(P.ctot, P.ts), dt, &re, &im);
       } else {
-        steering_coeff_fast(d, chc, P.k, dt, &re, &im);
+        steering_coeff_hw(d, chc, P.k, dt, &re, &im);
       }
       if (P.gain) apply_gain(P.gain[m * P.A + a], &re, &im);
     }
