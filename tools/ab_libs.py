@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from dpdk_dc_sand_amd import _lib, accel  # noqa: E402
 
-SHAPES = {"cfg3": (8, 4096, 256, 64, 16, 4096), "cfg4": (1, 4096, 256, 256, 64, 32768)}
+SHAPES = {"cfg2": (8, 4096, 256, 64, 1, 4096), "cfg3": (8, 4096, 256, 64, 16, 4096), "cfg4": (1, 4096, 256, 256, 64, 32768)}
 wl, flags, scale = sys.argv[1], int(sys.argv[2], 0), float(sys.argv[3])
 libs = []
 for spec in sys.argv[4:]:
