@@ -23,7 +23,8 @@ struct FusedArgs {
   long long base_ch;
   double ctot, ts, k, t0, batch_dt;
   float out_scale;
-  int knob;  // measurement knobs of the diagnostic build (0 in the product)
+  int knob;    // measurement knobs of the diagnostic build (0 in the product)
+  int ch_run;  // persistent kernels: consecutive channels per workgroup (set by their launcher)
 };
 
 // Per-(a, m) real beam weight applied to the float32 phasor (one rounding per component, as the oracle).

@@ -64,14 +64,17 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
               1064: "buffer loads, round-3 polynomial phasors", 128: "round-3 pair index math",
               1128: "buffer loads, round-3 pair index math", 1256: "buffer loads, prio contraction",
               1512: "buffer loads, prio phasors", 2024: "buffer loads, 16-pair model batches",
-              9192: "buffer loads, model loads pipelined, late voltages"}
+              9192: "buffer loads, model loads pipelined, late voltages",
+              20004: "persistent 1 wave/SIMD, ring 4", 20008: "persistent 1 wave/SIMD, ring 8",
+              20054: "persistent, ring 4, no-store", 20058: "persistent, ring 8, no-store"}
     if _os.environ.get("WIDE_MODES"):
         wnames = {int(m): wnames.get(int(m), str(m)) for m in _os.environ["WIDE_MODES"].split(",")}
     Ctot = int(_os.environ.get("DIAG_CTOT", "32768"))
     ref0 = None  # the first form's beams: every later form (tw) is compared with it too (22: both slabs per workgroup)
     for tw in [int(t) for t in _os.environ.get("WIDE_TW", "2,1").split(",")]:
         ref = None
-        full = [m for m in wnames if m % 1000 in (0, 64, 128) or (m >= 1000 and (m - 1000) & 8192)]
+        full = [m for m in wnames if m % 1000 in (0, 64, 128) or (1000 <= m < 20000 and (m - 1000) & 8192)
+                or 20000 <= m < 20050]
         for mode in full:  # float beams of the full forms against mode 0
             assert lib.bf_diag_wide(mode, tw, bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, B, C, T, A, M, Ctot, 1 / 1712e6,
                                     q.handle) == 0
