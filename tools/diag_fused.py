@@ -85,6 +85,14 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
                 ref0 = y
             print(f"  wide tw={tw} mode {mode:4d} vs mode {min(wnames)}: max |dy| {np.abs(y - ref).max():.3e} "
                   f"(max |y| {np.abs(ref).max():.3e}); vs the first form: max |dy| {np.abs(y - ref0).max():.3e}")
+            bad = np.argwhere(np.abs(y - ref).reshape(B, 2, C, T, 2 * M) > 1e-2)
+            if len(bad):
+                import collections
+                bb, pp, cc, tt, col = bad.T
+                for nm, v in {"pol": pp, "c%32": cc % 32, "c": cc, "t": tt, "t//64 (wave)": tt // 64,
+                              "t%64//4 (tl)": (tt % 64) // 4, "t%4 (i)": tt % 4, "col": col, "beam": col // 2}.items():
+                    cnt = collections.Counter(v.tolist())
+                    print(f"     {nm:14s} {len(cnt):5d} distinct; top {cnt.most_common(8)}")
         res = {m: [] for m in wnames}
         for r in range(int(_os.environ.get("DIAG_ROUNDS", "1"))):
             for mode in wnames:
