@@ -96,7 +96,10 @@ def test_q14_coeffs_large_delays(context, command_queue, tau_samples):
     (256, 40, 5, 208, 1, False, True), (256, 64, 6, 144, 2, True, False),
     # config 4's item shape, signed (64 beams, T = 256: the straight-line 8-step x 2-pass form at A = 256), and 3
     # k-steps (A = 96) with 64 beams
-    (256, 64, 12, 256, 1, True, False), (256, 64, 9, 256, 2, True, True), (96, 64, 7, 256, 1, True, False)])
+    (256, 64, 12, 256, 1, True, False), (256, 64, 9, 256, 2, True, True), (96, 64, 7, 256, 1, True, False),
+    # the LDS-DMA ring kernel (w32r: signed, 224 < A <= 256, T = 256, M % 32 == 0) with padded antennas in its last
+    # k-step (zero table entries, pulled-back loads), one and three 32-beam slabs, ragged channel runs
+    (240, 32, 11, 256, 2, True, False), (232, 96, 13, 256, 1, True, True), (248, 64, 21, 256, 1, True, False)])
 def test_fused_int8_table_path_equals_in_kernel_and_oracle(context, command_queue, A, M, C, T, B, signed, weighted):
     """The int8 wide path with the generated table (default) and with in-kernel phasors (coeff_table=False): the
     same bits, and the integer contract's."""
