@@ -1,6 +1,7 @@
 """GPU box: same-process A/B of one fused launch across several builds of libbf.so (e.g. an earlier round's tree
 built under build/ab_<tag>/): the same device buffers, interleaved rounds, median per library; the int8 outputs of
 every library are compared with the first one's (bitwise).
+(AB_DELAYS=ops: the ops benchmark's delay model.)
 usage: python tools/ab_libs.py <workload cfg3|cfg4> <flags> <scale> <tag=path/to/libbf.so> ..."""
 import ctypes
 import os
@@ -41,13 +42,17 @@ d[..., 0] = r.uniform(0, 10 * ts, (M, A))
 d[..., 1] = r.uniform(-1e-9, 1e-9, (M, A))
 d[..., 2] = r.uniform(-np.pi, np.pi, (M, A))
 d[..., 3] = r.uniform(-1, 1, (M, A))
+T0 = 1e-3
+if os.environ.get("AB_DELAYS") == "ops":  # tools/bench_ops.py's model: no rates, t0 = 0
+    d[..., 1] = d[..., 3] = 0.0
+    T0 = 0.0
 dv = accel.DeviceArray(ctx, (M * A * 4,), np.float32)
 dv.set(q, d.reshape(-1))
 bdt = T * 2 * Ctot * ts
 
 
 def launch(lib, i):
-    st = lib.bf_beamform_fused(xs[i % 2].ptr, dv.ptr, 1, ys[i % 2].ptr, B, C, T, A, M, Ctot, 0, ts, 1e-3, bdt, flags,
+    st = lib.bf_beamform_fused(xs[i % 2].ptr, dv.ptr, 1, ys[i % 2].ptr, B, C, T, A, M, Ctot, 0, ts, T0, bdt, flags,
                                scale, q.handle)
     if st != 0:
         raise RuntimeError(lib.bf_last_error().decode())
