@@ -572,7 +572,8 @@ def kernel_name(wl, out_int8, int8_contract="q14", coeff_table="on", signed=True
     """The launch's dominant kernel (bf_fused.hip dispatch): item kernels for A <= 64 and T <= 256, else the wide
     kernels; the int8 32-beam path with a coefficient table (A <= 256) is a table-driven contraction after its
     generator (q14_table_kernel, reported per step beside it): at config 4's shape with int8 samples the LDS-DMA
-    ring kernel (w32r: 224 < A <= 256, T = 256, M % 32 == 0), else the register-ring kernel (w32t)."""
+    ring kernel (w32r: 224 < A <= 256, T = 256, M % 32 == 0), else the register-ring kernel (w32t).  Float beams at
+    A = 256, T = 256, M % 32 == 0 (one delay model, no weights, fast coefficients): the persistent wide kernel."""
     integer = out_int8 and int8_contract == "q14"
     if wl["A"] <= 64 and wl["T"] <= 256:
         return "beamform_fused_i8_item_kernel" if integer else "beamform_fused_item_kernel"
@@ -582,6 +583,8 @@ def kernel_name(wl, out_int8, int8_contract="q14", coeff_table="on", signed=True
         if signed and 224 < wl["A"] <= 256 and wl["T"] == 256 and wl["M"] % 32 == 0:
             return "beamform_fused_i8_w32r_kernel"
         return "beamform_fused_i8_w32t_kernel"
+    if not out_int8 and wl["A"] == 256 and wl["T"] == 256 and wl["M"] % 32 == 0:
+        return "beamform_fused_wide_p2_kernel"
     return "beamform_fused_wide_kernel"
 
 

@@ -34,7 +34,7 @@ def test_realtime_factor_against_meerkat_ingest():
     ("cfg2", True, "q14", "on", "beamform_fused_i8_item_kernel"),
     ("cfg4", True, "q14", "on", "beamform_fused_i8_w32r_kernel"),
     ("cfg4", True, "q14", "off", "beamform_fused_i8_w32_kernel"),
-    ("cfg4", False, "q14", "on", "beamform_fused_wide_kernel")])
+    ("cfg4", False, "q14", "on", "beamform_fused_wide_p2_kernel")])
 def test_roofline_kernel_per_workload(workload, out_int8, contract, table, expected):
     assert bench.kernel_name(bench.WORKLOADS[workload], out_int8, contract, table) == expected
 

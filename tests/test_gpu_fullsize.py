@@ -159,6 +159,30 @@ def test_cfg4_shape_matches_oracle(context, command_queue, C, signed):
                           signed=signed)
 
 
+@pytest.mark.parametrize("M,C,B,signed,tau_samples", [
+    (32, 37, 1, True, 10), (96, 21, 2, False, 10), (64, 300, 1, True, 10), (64, 40, 1, True, 2e5)])
+def test_persistent_wide_kernel_shapes(context, command_queue, M, C, B, signed, tau_samples):
+    """The persistent float wide kernel (A = 256, T = 256, M % 32 == 0: beamform_fused_wide_p2_kernel) over its
+    channel runs: one and three 32-beam slabs, two batches (per-batch steering time, delay and phase rates), ragged
+    last runs (C = 37, 21, 300 over 256 CUs), uint8 samples, and delays of 2e5 samples (du ~ 3 revolutions a channel:
+    the float64 phase recurrence must not drift over a run).  Whole output within the fp32 tolerance of the oracle."""
+    A, T, Ctot, xeng = 256, 256, 32768, 3
+    raw = random_bytes((B, A, C, T, 2, 2), seed=M + C, signed=signed)
+    d = delay_model(M, A, seed=M + C)
+    d[..., 0] *= tau_samples / 10
+    t0, bdt = 2e-3, T * 2 * Ctot * TS
+    op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, sample_period=TS, delay_channels=1,
+                                 sample_signed=signed, t0=t0, batch_dt=bdt).instantiate(command_queue)
+    op.ensure_all_bound()
+    op.buffer("inSamples").set(command_queue, raw)
+    op.buffer("delay_vals").set(command_queue, d)
+    op()
+    y = op.buffer("outData").get(command_queue)
+    assert_beams_allclose(y, O.fused_beamform(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, signed=signed),
+                          O.reorder(raw), O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, t0=t0, batch_dt=bdt),
+                          signed=signed)
+
+
 def test_int8_overflow_bound_is_enforced(context, command_queue):
     """The Q14 path sums in int32: at unit gain |y| <= A * 255 * 23171 (uint8), so A = 363 is the largest uint8
     antenna count.  All-255 samples at zero phase hit the largest real part exactly; one antenna more is refused."""

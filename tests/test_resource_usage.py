@@ -79,3 +79,19 @@ def test_no_wide_store_data_hazard_in_product_kernels():
         total, hits = shc.scan(asm, window=2)
         bad += [f"{src}: {fn[:90]}: {st} / {n}" for fn, st, n, _ in hits]
     assert not bad, "\n".join(bad[:20])
+
+
+def test_no_inline_asm_result_reaches_an_mfma_unpadded():
+    """An inline-asm VGPR result read by an MFMA within two instructions of the statement needs the statement to end
+    in s_nop 1 (hipcc pads one state after an asm statement; VALU write -> MFMA operand read needs 2): the persistent
+    float kernel's uint8 form read a stale fragment in one accumulator without it (tools/store_hazard_check.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import store_hazard_check as shc
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        isas = dict(zip(SOURCES, ex.map(lambda s: shc.compile_isa(os.path.join(CSRC, s)), SOURCES)))
+    bad = [f"{src}: {fn[:90]}: {a} -> +{n} {m}" for src, asm in isas.items()
+           for fn, a, m, n in shc.scan_asm_to_mfma(asm, window=2)]
+    assert not bad, "\n".join(bad[:20])

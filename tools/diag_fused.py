@@ -74,7 +74,7 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
     for tw in [int(t) for t in _os.environ.get("WIDE_TW", "2,1").split(",")]:
         ref = None
         full = [m for m in wnames if m % 1000 in (0, 64, 128) or (1000 <= m < 20000 and (m - 1000) & 8192)
-                or 20000 <= m < 20050]
+                or 20000 <= m < 20050 or m in (20104, 20108)]
         for mode in full:  # float beams of the full forms against mode 0
             assert lib.bf_diag_wide(mode, tw, bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, B, C, T, A, M, Ctot, 1 / 1712e6,
                                     q.handle) == 0

@@ -4,6 +4,7 @@ keep the two apart: round 5 found a `buffer_store_dwordx4 v[80:83]` followed at 
 dword of lanes 12-15 of every row went out wrong in ~1e-5 of the bytes, varying run to run (tools/diag_w32r.py) --
 also the signature of round 4's unexplained w64h race.  This scans a source's device ISA for a VALU (or permlane
 swap) writing a wide store's data VGPRs within `window` instructions of it.
+Also: inline-asm results that reach an MFMA operand unpadded (scan_asm_to_mfma).
 usage: python tools/store_hazard_check.py <file.hip> [window] [extra hipcc flags]"""
 import re
 import subprocess
@@ -54,6 +55,51 @@ def scan(asm, window=2):
                     hits.append((fn, t, n, j))
                     break
     return total, hits
+
+
+def scan_asm_to_mfma(asm, window=2):
+    """Inline-asm VGPR results read by an MFMA within `window` instructions after the statement when the statement
+    does not end in an s_nop (hipcc pads one state after ;;#ASMEND; a VALU write -> MFMA SrcA/B/C read needs 2):
+    [(function, asm instruction, mfma, distance)]."""
+    fn, out = None, []
+    inside, dst, last, pending = False, set(), "", None
+    for line in asm.splitlines():
+        t = line.strip()
+        m = re.match(r"^(_Z\w+):", t)
+        if m:
+            fn, pending = m.group(1), None
+            continue
+        if t.startswith(";;#ASMSTART"):
+            inside, dst, last = True, set(), ""
+            continue
+        if t.startswith(";;#ASMEND"):
+            inside = False
+            padded = last.startswith("s_nop") and not last.startswith("s_nop 0")
+            pending = None if padded or not dst else [dst, 0, last]
+            continue
+        if not t or t.startswith((".", ";")) or t.endswith(":"):
+            continue
+        if inside:
+            last = t
+            if t.startswith("v_"):
+                parts = [x.rstrip(",") for x in t.split()[1:]]
+                if parts:
+                    dst |= _regs(parts[0])
+            continue
+        if pending is not None:
+            pending[1] += 1
+            if t.startswith("s_nop"):
+                pending = None
+                continue
+            if t.startswith("v_mfma"):
+                srcs = set()
+                for x in [x.rstrip(",") for x in t.split()[2:]]:
+                    srcs |= _regs(x)
+                if srcs & pending[0]:
+                    out.append((fn, pending[2], t, pending[1]))
+            if pending[1] >= window:
+                pending = None
+    return out
 
 
 def compile_isa(src, flags=()):
