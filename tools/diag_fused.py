@@ -254,7 +254,8 @@ if _os.environ.get("I8_AB"):  # interleaved A/B: int8 item kernel with uniform-b
         ts = sorted(ts)
         print(f"  i8 full, {form:8s} addressing  median {ts[len(ts) // 2] * 1e6:8.1f} us  min {ts[0] * 1e6:8.1f} us")
 names_f8 = {0: "full (f32 contract)", 1: "no-coef", 2: "no-mfma", 4: "no-store", 5: "no-coef,no-store", 8: "no-load",
-            128: "cached loads", 64: "occ 4 bound", 96: "occ 3 bound", 16: "exact coef, occ 4", 80: "exact coef"}
+            128: "cached loads", 64: "occ 4 bound", 96: "occ 3 bound", 16: "exact coef, occ 4", 80: "exact coef",
+            65: "occ 4, no-coef", 68: "occ 4, no-store", 69: "occ 4, no-coef,no-store", 72: "occ 4, no-load"}
 names_fs = {0: "staged 1 KiB f32 stores", 4: "staged, no-store", 128: "staged, cached loads", 256: "staged, nt stores",
             384: "staged, cached loads, nt st", 192: "staged, cached, occ 3"}
 for kbase, kname in ((32, "item"), (512, "i8"), (8192, "f8"), (16384, "fs")):
