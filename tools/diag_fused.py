@@ -98,6 +98,17 @@ if "wide" in _os.environ.get("DIAG_KERNELS", ""):
             for mode in wnames:
                 res[mode].append(timeit(lambda i: lib.bf_diag_wide(mode, tw, bufs[i % 2][0].ptr, dv.ptr, bufs[i % 2][1].ptr,
                                                                    B, C, T, A, M, Ctot, 1 / 1712e6, q.handle)))
+        for mode in [m for m in wnames if 20100 <= m < 150000 and ((m - 20100) // 10) & 4096]:
+            # the persistent kernel's phase stamps (Mode 4096): per-wave s_memtime sums over the output's first bytes
+            assert lib.bf_diag_wide(mode, tw, bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, B, C, T, A, M, Ctot, 1 / 1712e6,
+                                    q.handle) == 0
+            st = bufs[0][1].get(q).view(np.uint64)[1 << 24:(1 << 24) + 256 * 8 * 4].reshape(-1, 4).astype(np.float64)
+            st = st[st[:, 3] > 0]
+            tot = st[:, :3].sum(1)
+            print(f"  wide stamps mode {mode}: per wave {tot.mean():.0f} clocks over {st[:, 3].mean():.1f} channels: "
+                  f"steps {st[:, 0].mean() / tot.mean():.3f}, store issue {st[:, 1].mean() / tot.mean():.3f}, "
+                  f"barrier {st[:, 2].mean() / tot.mean():.3f}; per channel steps {st[:, 0].mean() / st[:, 3].mean():.0f}, "
+                  f"stores {st[:, 1].mean() / st[:, 3].mean():.0f}, barrier {st[:, 2].mean() / st[:, 3].mean():.0f}")
         for mode in wnames:
             ts = sorted(res[mode])
             print(f"  wide tw={tw} mode {mode:2d} {wnames[mode]:18s} median {ts[len(ts) // 2] * 1e6:8.1f} us  "
