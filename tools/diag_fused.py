@@ -289,6 +289,16 @@ for kbase, kname in ((32, "item"), (512, "i8"), (8192, "f8"), (16384, "fs")):
                   else (names_fs[mode], alg) if kname == "fs" else (names[mode], alg))
         print(f"  {kname} mode {mode:3d} {nm:18s} median {med*1e6:8.1f} us  min {mn*1e6:8.1f} us  "
               f"alg {ab/med/1e9:7.1f} GB/s  ({len(ts)} rounds)")
+if _os.environ.get("DIAG_F8_CMP"):  # int8-via-f32 variants against the product order, bitwise (int8 beams)
+    outs = {}
+    for mode in [int(m) for m in _os.environ["DIAG_F8_CMP"].split(",")]:
+        assert lib.bf_diag_fused(8192 + mode, bufs[0][0].ptr, dv.ptr, bufs[0][1].ptr, B, C, T, A, M, C, 1 / 1712e6,
+                                 q.handle) == 0
+        outs[mode] = bufs[0][1].get(q)[:B * 2 * C * T * 2 * M].copy()
+    ref_mode = min(outs)
+    for mode, o in outs.items():
+        n = int(np.count_nonzero(o != outs[ref_mode]))
+        print(f"  f8 mode {mode} vs mode {ref_mode}: {n} of {o.size} int8 beams differ", flush=True)
 if _os.environ.get("DIAG_MIX"):  # the int8 path's 4:1 read:write mix, uniformly interleaved
     for grid in (1024, 2048, 4096, 8192, 16384):
         for code, nm in ((200, "nt load+store"), (201, "nt load")):
