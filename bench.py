@@ -429,26 +429,44 @@ def pmc_traffic(args):
     if not os.path.exists(exe):
         return None, "rocprofv3 not found"
     vals = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+    # third pass: the matrix pipe's busy cycles (summed over the 1024 SIMDs) and the GPU-active cycles (summed over
+    # the 8 XCDs), for the measured MFMA-busy fraction and the clock the chip held (MI355X_MICROARCH.md, DVFS)
+    for counters in (("FETCH_SIZE",), ("WRITE_SIZE",), ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE")):
         out = tempfile.mkdtemp(prefix="bfpmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+        cmd = [exe, "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
                "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--output", args.output,
                "--int8-contract", args.int8_contract] + (["--unsigned"] if args.unsigned else [])
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
         if r.returncode != 0 or not files:
-            return None, f"rocprofv3 {counter} failed rc={r.returncode}: {r.stderr[-300:]}"
-        per = []
-        with open(files[0]) as f:
-            for row in csv.DictReader(f):
-                if "beamform_fused" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                    per.append(float(row["Counter_Value"]))
-        if not per:
-            return None, f"no {counter} rows for the fused kernel"
-        vals[counter] = sorted(per)[len(per) // 2]
+            if counters[0].startswith("SQ_"):  # informational pass: the traffic above stands without it
+                break
+            return None, f"rocprofv3 {counters[0]} failed rc={r.returncode}: {r.stderr[-300:]}"
+        for counter in counters:
+            per = []
+            with open(files[0]) as f:
+                for row in csv.DictReader(f):
+                    if "beamform_fused" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                        per.append(float(row["Counter_Value"]))
+            if not per:
+                if counter.startswith(("SQ_", "GRBM_")):
+                    continue
+                return None, f"no {counter} rows for the fused kernel"
+            vals[counter] = sorted(per)[len(per) // 2]
     traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
     return traffic, vals
+
+
+def pmc_mfma_busy(vals, kernel_s):
+    """The measured matrix-pipe busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x the kernel's GPU-active
+    cycles, GRBM_GUI_ACTIVE / 8 XCDs) and the clock the chip held (those cycles over the event-timed launch)."""
+    if not isinstance(vals, dict) or "SQ_VALU_MFMA_BUSY_CYCLES" not in vals or not vals.get("GRBM_GUI_ACTIVE"):
+        return None
+    cycles = vals["GRBM_GUI_ACTIVE"] / 8.0
+    return {"busy_frac": round(vals["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cycles), 4),
+            "clock_GHz": round(cycles / kernel_s / 1e9, 3),
+            "counters": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), profiled pass"}
 
 
 ADC_SAMPLE_RATE, FFT_SIZE = 1712e6, 8192  # MeerKAT L-band (BeamformerParameters.h:15-16)
@@ -728,6 +746,9 @@ def main():
             traffic, info = pmc_traffic(args)
             line["roofline"]["traffic"] = traffic
             line["roofline"]["traffic_counters"] = info
+            busy = pmc_mfma_busy(info, r["kernel_s"])
+            if busy and isinstance(line.get("mfma"), dict):
+                line["mfma"]["pmc"] = busy
         except Exception as e:
             line["roofline"]["traffic_counters"] = f"unavailable: {str(e)[:200]}"
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:

@@ -104,3 +104,14 @@ def test_mfma_block_and_contraction_split():
     one = {"avg_launch_us": 620.0, "mfma": f}
     bench.mfma_split(one, {"avg_us": 620.0})  # one kernel per step: nothing to split
     assert "contraction_only" not in one["mfma"]
+
+
+def test_pmc_mfma_busy():
+    # the persistent f32 kernel's PMC (profiles/r5_f3_cfg4_wide_pmc.txt): 5.37e8 busy cycles over 1024 SIMDs and
+    # 9.21e6 GPU-active cycles over 8 XCDs -> 45.5 % busy; no SQ pass -> None
+    b = bench.pmc_mfma_busy({"FETCH_SIZE": 1.0, "WRITE_SIZE": 1.0, "SQ_VALU_MFMA_BUSY_CYCLES": 5.37e8,
+                             "GRBM_GUI_ACTIVE": 9.21e6}, 589.6e-6)
+    assert b["busy_frac"] == pytest.approx(0.4555, abs=1e-4)
+    assert b["clock_GHz"] == pytest.approx(1.953, abs=1e-3)
+    assert bench.pmc_mfma_busy({"FETCH_SIZE": 1.0, "WRITE_SIZE": 1.0}, 1e-3) is None
+    assert bench.pmc_mfma_busy("unavailable", 1e-3) is None
