@@ -419,41 +419,54 @@ def cpu_baseline(wl, out_int8, seconds=10.0):
                       f"BLAS threads={threads})"}
 
 
+def pmc_pass(args, counters, workload, output, contract):
+    """One rocprofv3 --pmc pass over a short child run of the fused launch (3 timed + 1 warm-up dispatches): the
+    median per-dispatch value of each counter over the `beamform_fused*` kernels, or (None, error)."""
+    exe = "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, "rocprofv3 not found"
+    out = tempfile.mkdtemp(prefix="bfpmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = [exe, "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+           sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", workload,
+           "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--output", output,
+           "--int8-contract", contract] + (["--unsigned"] if args.unsigned else [])
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+    if r.returncode != 0 or not files:
+        return None, f"rocprofv3 {' '.join(counters)} failed rc={r.returncode}: {r.stderr[-300:]}"
+    vals = {}
+    for counter in counters:
+        per = []
+        with open(files[0]) as f:
+            for row in csv.DictReader(f):
+                if "beamform_fused" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    per.append(float(row["Counter_Value"]))
+        if not per:
+            return None, f"no {counter} rows for the fused kernel"
+        vals[counter] = sorted(per)[len(per) // 2]
+    return vals, None
+
+
+MFMA_COUNTERS = ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE")
+
+
 def pmc_traffic(args):
     """HBM bytes per fused launch from rocprofv3 counters: FETCH_SIZE and WRITE_SIZE in separate passes
     (MI355X_MICROARCH.md: gfx950 FETCH_SIZE reads 1/2 of a wide coalesced stream -> x2; WRITE_SIZE exact; KiB).
     Calibrated in-repo (tools/pmc_calibrate.py, profiles/r2_v_pmc_calibration.jsonl): a 1 GiB streaming read gives
     FETCH_SIZE = 0.500 x the bytes (every request a 128-byte TCC_EA0_RDREQ_128B, tallied at 64 B), a 1 GiB write
-    WRITE_SIZE = 1.000 x, and a 1 GiB + 256 MiB mix the same two ratios."""
-    exe = "/opt/rocm/bin/rocprofv3"
-    if not os.path.exists(exe):
-        return None, "rocprofv3 not found"
+    WRITE_SIZE = 1.000 x, and a 1 GiB + 256 MiB mix the same two ratios.  A third pass takes the matrix pipe's busy
+    cycles (summed over the 1024 SIMDs) and the GPU-active cycles (summed over the 8 XCDs): the measured MFMA-busy
+    fraction and the clock the chip held (MI355X_MICROARCH.md, DVFS); it is informational."""
     vals = {}
-    # third pass: the matrix pipe's busy cycles (summed over the 1024 SIMDs) and the GPU-active cycles (summed over
-    # the 8 XCDs), for the measured MFMA-busy fraction and the clock the chip held (MI355X_MICROARCH.md, DVFS)
-    for counters in (("FETCH_SIZE",), ("WRITE_SIZE",), ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE")):
-        out = tempfile.mkdtemp(prefix="bfpmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [exe, "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
-               sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
-               "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--output", args.output,
-               "--int8-contract", args.int8_contract] + (["--unsigned"] if args.unsigned else [])
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
-        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
-        if r.returncode != 0 or not files:
-            if counters[0].startswith("SQ_"):  # informational pass: the traffic above stands without it
-                break
-            return None, f"rocprofv3 {counters[0]} failed rc={r.returncode}: {r.stderr[-300:]}"
-        for counter in counters:
-            per = []
-            with open(files[0]) as f:
-                for row in csv.DictReader(f):
-                    if "beamform_fused" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                        per.append(float(row["Counter_Value"]))
-            if not per:
-                if counter.startswith(("SQ_", "GRBM_")):
-                    continue
-                return None, f"no {counter} rows for the fused kernel"
-            vals[counter] = sorted(per)[len(per) // 2]
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        v, err = pmc_pass(args, (counter,), args.workload, args.output, args.int8_contract)
+        if err:
+            return None, err
+        vals.update(v)
+    v, err = pmc_pass(args, MFMA_COUNTERS, args.workload, args.output, args.int8_contract)
+    if not err:
+        vals.update(v)
     traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
     return traffic, vals
 
@@ -749,6 +762,17 @@ def main():
             busy = pmc_mfma_busy(info, r["kernel_s"])
             if busy and isinstance(line.get("mfma"), dict):
                 line["mfma"]["pmc"] = busy
+            # config 4 (the MFMA-heavy shape): the same measured busy fraction for its secondary lines' kernels
+            for sec in line.get("secondary", []):
+                if "error" in sec or not sec["workload"].startswith("cfg4") or not isinstance(sec.get("mfma"), dict):
+                    continue
+                out_int8 = sec["output"].startswith("int8")
+                contract = "f32" if "requantised" in sec["output"] else "q14"
+                v, err = pmc_pass(args, MFMA_COUNTERS, "cfg4", "int8" if out_int8 else "f32", contract)
+                # the counters cover the beamform_fused* kernel only: the int8 line's contraction, not its generator
+                kernel_us = sec["mfma"].get("contraction_only", {}).get("kernel_us", sec["avg_launch_us"])
+                busy = None if err else pmc_mfma_busy(v, kernel_us * 1e-6)
+                sec["mfma"]["pmc"] = busy or {"error": err or "no counters"}
         except Exception as e:
             line["roofline"]["traffic_counters"] = f"unavailable: {str(e)[:200]}"
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
