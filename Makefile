@@ -11,8 +11,16 @@ SRCS     := $(CSRC)/bf_runtime.cpp $(CSRC)/bf_coeff.hip $(CSRC)/bf_reorder.hip $
 OBJS     := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 HDRS     := $(wildcard $(CSRC)/*.hpp) $(wildcard $(CSRC)/diag/*.inc) include/bf.h
 
-.PHONY: all clean diag cabi
+.PHONY: all clean diag cabi stream
 all: $(LIB) cabi
+
+# bench.py's stream ceiling (the box's best plain stream over a kernel's byte mix): a small library of its own, so the
+# GPU box needs no diagnostic build.
+STREAM_LIB := build/libbf_stream.so
+stream: $(STREAM_LIB)
+$(STREAM_LIB): tools/stream_ceiling.hip $(CSRC)/diag/stream_kernels.hpp
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
 # C callers of the ABI (tests/test_c_abi.py): the harness-order smoke and INTEGRATION.md's streaming example,
 # compiled from the markdown block itself.  Plain C against include/bf.h, linked to the in-tree libbf.so.

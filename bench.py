@@ -3,6 +3,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg2|cfg4] [--no-cpu-baseline] [--no-pmc]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
+`--gpus N` alone starts the N ranks itself (N child processes of this script, one per GPU, RANK / WORLD_SIZE /
+MASTER_* set; the parent never touches a GPU); under an external launcher `--gpus` must equal WORLD_SIZE.
+
 A "step" is one pass of the hot path over one batch block of synthetic input already resident in HBM: one
 `bf_beamform_fused` launch = pre-beamform reorder (fused) + per-batch steering-coefficient regeneration from the
 delay model + the antenna x beam complex contraction, for every (batch, pol, channel, sample) of the shard.
@@ -27,7 +30,9 @@ launch duration from HIP events on the launch stream; `roofline.read_frac` = the
 peak (the north star's "HBM-read roofline"), and `read_frac_ceiling` the same for this box's plain streaming kernel
 over the kernel's whole read + write byte mix: the read fraction the beams' writes leave reachable.  `roofline.traffic` = HBM bytes per launch from rocprofv3 PMC
 counters (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate passes), rank 0, N = 1.  `ceiling` = the same
-traffic mix as a plain streaming kernel on this box (diagnostic library), when it is built.
+traffic mix as a plain streaming kernel on this box (build/libbf_stream.so), with `target_reachable`: whether the
+north star's 0.70 of 8 TB/s is within that stream for the byte mix.  A `kind: streaming` secondary (rank 0, N = 1) is
+config 5: 256 MiB frames through the native pinned-ring pipeline against this process's own H2D copy rate.
 `cpu_baseline` = the oracle's vectorised NumPy restatement on a bounded channel sample, rank 0, N = 1.
 """
 import argparse
@@ -58,9 +63,11 @@ WORKLOADS = {
 }
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU).  Without an external launcher, N > 1 starts N child ranks of this script "
+                        "itself; under torch.distributed.run it must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
@@ -86,6 +93,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-secondary", action="store_true")
+    p.add_argument("--no-stream", action="store_true",
+                   help="skip the config-5 streaming secondary (host ring -> H2D -> fused -> D2H, rank 0, N = 1)")
+    p.add_argument("--stream-frames", type=int, default=64, help="timed frames of the config-5 streaming secondary")
     p.add_argument("--no-ceiling", action="store_true")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the rocprofv3 --kernel-trace re-run that checks the event timings (rank 0, N = 1)")
@@ -93,13 +103,93 @@ def parse():
                    help="directory for that re-run's trace, timed_kernel_stats.csv and prof_bench.json")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--prof-child", action="store_true", help=argparse.SUPPRESS)
-    a = p.parse_args()
+    p.add_argument("--rank-probe", action="store_true", help=argparse.SUPPRESS)  # CPU test of the rank launch
+    a = p.parse_args(argv)
     if a.out_f32:
         a.output = "f32"
     if a.out_int8:
         a.output = "int8"
     a.out_int8 = a.output == "int8"
     return a
+
+
+def resolve_world(args, env=None):
+    """The ranks of this invocation (one process per GPU, rank r = X-engine r).  Returns (world, launch):
+    `launch` is True when this process must start the ranks itself (`--gpus N > 1` and no external launcher, i.e. no
+    WORLD_SIZE in the environment).  Under an external launcher (torch.distributed.run) `--gpus` must equal WORLD_SIZE:
+    a mismatch would silently time a different number of ranks than the command line names."""
+    env = os.environ if env is None else env
+    if env.get("WORLD_SIZE") is not None:
+        world = int(env["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            raise ValueError(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        args.gpus = world
+        return world, False
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise ValueError(f"--gpus must be >= 1, got {n}")
+    args.gpus = n
+    return n, n > 1
+
+
+def free_port_pair(host="127.0.0.1", tries=64):
+    """A port p with p and p + 1 both free on `host` (the rendezvous group listens on MASTER_PORT + 1)."""
+    import socket
+    for _ in range(tries):
+        s = socket.socket()
+        s.bind((host, 0))
+        p = s.getsockname()[1]
+        t = socket.socket()
+        try:
+            t.bind((host, p + 1))
+            return p
+        except OSError:
+            continue
+        finally:
+            t.close()
+            s.close()
+    raise RuntimeError("no free port pair for the rank rendezvous")
+
+
+def launch_ranks(n, argv, poll_s=0.05, grace_s=20.0):
+    """`bench.py --gpus N` with no launcher: start N fresh child processes of this script, one per GPU, with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set -- the reference's one worker per device
+    (utilities/pcie_bandwidth_tests/main.cpp:214-224), each rank X-engine `rank` (coeff_generator.py:53).  This
+    process never touches the GPU; the children inherit stdout, so rank 0's JSON line is the run's output.  If a rank
+    fails, the others are stopped (they would wait in a collective) and its exit status is returned."""
+    port = free_port_pair()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BF_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env, cwd=ROOT))
+    rc = 0
+    try:
+        pending = list(range(n))
+        while pending and rc == 0:
+            for r in list(pending):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                pending.remove(r)
+                if c != 0:
+                    rc = c if c > 0 else 128 - c  # a signal -> the shell's 128 + signal
+                    print(f"bench.py: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr,
+                          flush=True)
+                    break
+            time.sleep(poll_s)
+    finally:
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.terminate()
+        deadline = time.monotonic() + grace_s
+        for p in live:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc
 
 
 class Dist:
@@ -312,18 +402,19 @@ def contract_check(args, dist, wl, r):
 
 
 def stream_ceiling(args, in_bytes, out_bytes):
-    """The same traffic mix (in_bytes read, out_bytes written) as plain streaming kernels from the diagnostic
-    library (build/libbf_diag.so: 16-byte lanes, plain / non-temporal loads and stores, 4:1 interleaved mix for
-    the int8 path): the best of them is this box's achievable ceiling for the fused kernel's traffic."""
+    """The same traffic mix (in_bytes read, out_bytes written) as plain streaming kernels from the stream-ceiling
+    library (build/libbf_stream.so, tools/stream_ceiling.hip: 16-byte lanes, plain / non-temporal loads and stores,
+    4:1 interleaved mix for the int8 path): the best of them is this box's achievable ceiling for the fused kernel's
+    traffic."""
     import ctypes
 
     from dpdk_dc_sand_amd import accel
-    path = os.path.join(ROOT, "build", "libbf_diag.so")
+    path = os.path.join(ROOT, "build", "libbf_stream.so")
     if not os.path.exists(path):
         return None
     lib = ctypes.CDLL(path)
     V, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
-    lib.bf_diag_stream.argtypes = [V, V, S, S, I, I, V]
+    lib.bf_stream_ceiling.argtypes = [V, V, S, S, I, I, V]
     bufs = [(accel.DeviceArray(args.ctx, (in_bytes,), "u1"), accel.DeviceArray(args.ctx, (max(out_bytes, 16),), "u1"))
             for _ in range(2)]
     best = None
@@ -333,21 +424,92 @@ def stream_ceiling(args, in_bytes, out_bytes):
     for grid in (1024, 2048):
         for code in codes:
             for i in range(3):
-                lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, in_bytes, out_bytes, grid, code,
-                                   args.queue.handle)
+                lib.bf_stream_ceiling(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, in_bytes, out_bytes, grid, code,
+                                      args.queue.handle)
             e0 = accel.Event(args.queue)
             n = 10
             for i in range(n):
-                lib.bf_diag_stream(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, in_bytes, out_bytes, grid, code,
-                                   args.queue.handle)
+                lib.bf_stream_ceiling(bufs[i % 2][0].ptr, bufs[i % 2][1].ptr, in_bytes, out_bytes, grid, code,
+                                      args.queue.handle)
             e1 = accel.Event(args.queue)
             args.queue.finish()
             t = e1.time_since(e0) / n
             if best is None or t < best[0]:
                 best = (t, grid, code)
     return {"us": round(best[0] * 1e6, 2), "GBps": round((in_bytes + out_bytes) / best[0] / 1e9, 1),
-            "kernel": f"bf_diag_stream grid {best[1]} mode {best[2]}",
+            "kernel": f"bf_stream_ceiling grid {best[1]} mode {best[2]}",
             "note": "best plain streaming kernel over the same read/write byte mix on this box"}
+
+
+def copy_rate(args, host, direction, reps=8):
+    """GB/s of bf_memcpy_{h2d,d2h} between a pinned host array and a device buffer on one stream (this process)."""
+    import numpy as np
+
+    from dpdk_dc_sand_amd import _lib, accel
+    dev = accel.DeviceArray(args.ctx, (host.nbytes,), np.uint8)
+    fn = "bf_memcpy_h2d" if direction == "h2d" else "bf_memcpy_d2h"
+    ptrs = (dev.ptr, host.ctypes.data) if direction == "h2d" else (host.ctypes.data, dev.ptr)
+    _lib.call(fn, *ptrs, host.nbytes, args.queue.handle)
+    args.queue.finish()
+    t = time.perf_counter()
+    for _ in range(reps):
+        _lib.call(fn, *ptrs, host.nbytes, args.queue.handle)
+    args.queue.finish()
+    return host.nbytes * reps / (time.perf_counter() - t) / 1e9
+
+
+def stream_secondary(args, depth=4):
+    """Config 5 (BASELINE configs[4]): the sustained rate of host frames through the native streaming pipeline
+    (bf_pipeline: pinned host ring -> H2D stream -> fused coefficient regeneration + beamform + int8 requantisation ->
+    D2H stream, `depth` frames in flight), against this process's own pinned H2D copy rate on the same buffers -- the
+    PCIe bound, since a frame's voltages (256 MiB) are 4x its int8 beams.  The reference moves the same data in
+    back-to-back phases (common/UnitTest.cpp:28-57; cudaPcieRateTest.cpp:63-123)."""
+    import numpy as np
+
+    from dpdk_dc_sand_amd import accel
+    from dpdk_dc_sand_amd.beamforming import StreamingBeamformerTemplate
+    A, M, C, T, B = 64, 16, 4096, 256, 1
+    tmpl = StreamingBeamformerTemplate(args.ctx, B, C, C, T, A, M, delay_channels=1, sample_signed=True,
+                                       out_int8=True, out_scale=1 / 64, batch_dt=T * 2 * C * TS, depth=depth)
+    rng = np.random.default_rng(11)
+    frames = []
+    for _ in range(depth):
+        h = accel.HostArray(tmpl.input_shape, np.int8, args.ctx)
+        h[...] = np.frombuffer(rng.bytes(h.nbytes), np.int8).reshape(h.shape)
+        frames.append(h)
+    beams = [accel.HostArray(tmpl.output_shape, np.int8, args.ctx) for _ in range(depth)]
+    h2d = copy_rate(args, frames[0], "h2d")
+    d2h = copy_rate(args, frames[1 % depth], "d2h")
+    d = delay_model(np, rng, tmpl.delay_shape)
+    with tmpl.instantiate() as sb:
+        sb.set_delays(d)
+        for k in range(2 * depth):  # warm-up: pipeline, clocks
+            sb.submit(frames[k % depth], beams[k % depth])
+        sb.flush()
+        tickets = []
+        t = time.perf_counter()
+        for k in range(args.stream_frames):
+            if k >= depth:
+                sb.wait(tickets[k - depth])
+            tickets.append(sb.submit(frames[k % depth], beams[k % depth]))
+        sb.wait(tickets[-1])
+        dt = time.perf_counter() - t
+        stages = np.array([sb.stage_ms(tk) for tk in tickets[-depth:]])
+    samples = A * 2 * C * T * B * args.stream_frames
+    rate = samples / dt / 1e9
+    bound = h2d / 2  # 2 bytes per complex 8-bit sample
+    return {"workload": "cfg5: streaming ingest, config-3 frames (64 ants, 16 beams, 4096 ch, T=256, B=1: 256 MiB "
+                        "int8 voltages in, 64 MiB int8 beams out) through the pinned host ring (BASELINE configs[4])",
+            "kind": "streaming", "output": "int8", "value": round(rate, 2), "unit": "Gsamples/s", "n_gpus": 1,
+            "frames": args.stream_frames, "depth": depth, "seconds": round(dt, 4),
+            "frames_per_s": round(args.stream_frames / dt, 1),
+            "pcie_copy_GBps": {"h2d": round(h2d, 2), "d2h": round(d2h, 2),
+                               "note": "bf_memcpy_{h2d,d2h} of one pinned 256 MiB frame, one stream, this process"},
+            "h2d_bound_Gsamples_s": round(bound, 2), "frac_of_h2d_bound": round(rate / bound, 4),
+            "stage_ms_median": {"h2d": round(float(np.median(stages[:, 0])), 3),
+                                "compute": round(float(np.median(stages[:, 1])), 3),
+                                "d2h": round(float(np.median(stages[:, 2])), 3)},
+            "pipeline": "bf_pipeline (csrc/bf_pipeline.cpp): H2D / compute / D2H HIP streams, per-slot events"}
 
 
 def host_cpus():
@@ -514,7 +676,7 @@ def rocprof_check(args, n_secondary):
            os.path.abspath(__file__), "--prof-child", "--workload", args.workload, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--settle-ms", str(args.settle_ms), "--output", args.output,
            "--int8-contract", args.int8_contract, "--coeff-table", args.coeff_table, "--no-pmc", "--no-cpu-baseline",
-           "--no-ceiling"]
+           "--no-ceiling", "--no-stream"]
     cmd += (["--unsigned"] if args.unsigned else []) + (["--no-secondary"] if n_secondary == 0 else [])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT)
     files = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
@@ -635,19 +797,48 @@ def secondary(args, dist, workload, out_int8, int8_contract="q14"):
            "read_frac": round(r["read_bytes"] / r["kernel_s"] / 1e9 / HBM_PEAK_GBS, 4),
            "avg_launch_us": round(r["kernel_s"] * 1e6, 2), "alg_bytes_per_launch": r["alg_bytes"],
            "mfma": mfma_util(wl, out_int8, int8_contract, r["kernel_s"])}
+    if dist.group:  # every rank's own launch time (each rank its own X-engine's channels)
+        out["per_rank_avg_launch_us"] = dist.group.gather_json(round(r["kernel_s"] * 1e6, 2))
     if not args.no_ceiling and dist.world == 1:
         ceil = stream_ceiling(args, r["read_bytes"], int(r["alg_bytes"] - r["read_bytes"]))
         if ceil:
             out["ceiling"] = ceil
             out["frac_of_ceiling"] = round(ceil["us"] / out["avg_launch_us"], 4)
             out["read_frac_ceiling"] = round(r["read_bytes"] / (ceil["us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+            out.update(target_block(r["alg_bytes"], ceil["us"]))
     return out
+
+
+NORTH_STAR_FRAC = 0.70  # BASELINE.json north_star: >= 70 % of the HBM roofline at 1 GPU
+
+
+def target_block(alg_bytes, ceiling_us, target=NORTH_STAR_FRAC):
+    """Whether the north star's 0.70 of 8 TB/s is reachable for this byte mix on this box: `ceiling_frac` is the
+    roofline fraction a kernel running exactly at the box's best plain stream over the same read/write bytes would
+    show; `target_needs_frac_of_ceiling` what fraction of that stream the target asks for (> 1: above any stream)."""
+    ceiling_frac = alg_bytes / (ceiling_us * 1e-6) / 1e9 / HBM_PEAK_GBS
+    return {"target_frac": target, "ceiling_frac": round(ceiling_frac, 4),
+            "target_reachable": bool(ceiling_frac >= target),
+            "target_needs_frac_of_ceiling": round(target / ceiling_frac, 4)}
 
 
 def main():
     args = parse()
+    world, launch = resolve_world(args)
+    if launch:  # before anything touches the GPU: this process only starts and waits for the ranks
+        sys.exit(launch_ranks(world, sys.argv[1:]))
     wl = WORKLOADS[args.workload]
     dist = Dist(args.scatter_backend, force=args.scatter_at_one)
+    if args.rank_probe:  # the ranks' rendezvous and timing-bracket collectives only, no GPU (tests/test_bench_logic.py)
+        dist.barrier()
+        top = dist.max(float(dist.rank))
+        got = dist.group.gather_json({"rank": dist.rank, "local_rank": dist.local_rank}) if dist.group else \
+            [{"rank": 0, "local_rank": 0}]
+        if dist.rank == 0:
+            print(json.dumps({"n_gpus": dist.world, "gpus_arg": args.gpus, "max_rank": top, "ranks": got,
+                              "ranks_launched_by": os.environ.get("BF_BENCH_LAUNCHER")}), flush=True)
+        dist.close()
+        return
     from dpdk_dc_sand_amd import accel
 
     n_dev = accel.device_count()
@@ -688,7 +879,9 @@ def main():
                    "n_channels_per_gpu": wl["C"], "n_samples_per_channel": wl["T"], "n_batches": wl["B"],
                    "n_pols": 2, "output": "int8" if args.out_int8 else "float32",
                    "int8_contract": args.int8_contract if args.out_int8 else None,
-                   "parallelism": f"channel-shard x{dist.world} (xeng_id = rank), no data-path collective"},
+                   "parallelism": f"channel-shard x{dist.world} (xeng_id = rank), no data-path collective",
+                   "ranks_launched_by": os.environ.get("BF_BENCH_LAUNCHER") or
+                   ("external launcher (WORLD_SIZE)" if "WORLD_SIZE" in os.environ else "single process")},
         "beams_per_s": round(r["beams_per_step"] * args.steps * dist.world / r["t_max"], 1),
         "compute": compute_desc(args.out_int8, args.int8_contract),
         "device": args.ctx.device.name,
@@ -706,6 +899,8 @@ def main():
         "realtime": realtime(wl, dist.world, value),
         "cpu_baseline": None,
     }
+    if dist.group:
+        line["per_rank_avg_launch_us"] = dist.group.gather_json(round(r["kernel_s"] * 1e6, 2))
     if dist.rank == 0 and dist.world == 1 and args.out_int8 and args.int8_contract == "q14" and not args.prof_child:
         line["int8_contract_check"] = contract_check(args, dist, wl, r)
     r.pop("ops")
@@ -717,6 +912,7 @@ def main():
             # the north star's "HBM-read roofline": with the beams written too, a read-only fraction of 1 is not
             # reachable; the best this box allows is the voltage bytes over its own stream time for the same mix
             line["roofline"]["read_frac_ceiling"] = round(r["read_bytes"] / (ceil["us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+            line["roofline"].update(target_block(r["alg_bytes"], ceil["us"]))
     if not args.no_secondary and args.workload == "cfg3":
         # every rank runs the secondaries (each is timed between barriers, max over ranks); at N > 1 config 4
         # channel-sharded: 4096 channels per rank of the 32768-channel band (BASELINE configs[3] at N = 8)
@@ -733,8 +929,15 @@ def main():
                 line["secondary"].append(secondary(args, dist, workload, out_int8, contract))
             except Exception as e:  # secondary lines are informational
                 line["secondary"].append({"workload": workload, "error": str(e)[:200]})
+    if dist.rank == 0 and dist.world == 1 and not (args.no_stream or args.prof_child):
+        try:
+            line.setdefault("secondary", []).append(stream_secondary(args))
+        except Exception as e:  # noqa: BLE001 -- informational
+            line.setdefault("secondary", []).append({"workload": "cfg5", "kind": "streaming",
+                                                     "error": f"{type(e).__name__}: {str(e)[:200]}"})
     if dist.rank == 0 and dist.world == 1 and not (args.no_rocprof or args.prof_child):
-        secs = [s for s in line.get("secondary", []) if "error" not in s]
+        # the timed regions of the profiled child: the headline, then each device-resident secondary in order
+        secs = [s for s in line.get("secondary", []) if "error" not in s and s.get("kind") != "streaming"]
         try:
             regions, child, err = rocprof_check(args, len(secs))
         except Exception as e:  # informational: the live event timing above is the measurement

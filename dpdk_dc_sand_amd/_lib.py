@@ -85,6 +85,8 @@ PROTOTYPES = {
     "bf_channel_scatter": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "bf_comm_stats": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]),
     "bf_comm_load": (c_int, []),
+    "bf_scatter_plan": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_size_t, c_void_p, c_size_t,
+                                ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)]),
     "bf_checksum": (c_int, [c_void_p, c_size_t, c_size_t, c_size_t, ctypes.POINTER(ctypes.c_ulonglong), c_void_p]),
     "bf_fill_random": (c_int, [c_void_p, c_size_t, ctypes.c_ulonglong, c_void_p]),
 }

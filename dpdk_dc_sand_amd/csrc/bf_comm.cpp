@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "bf_common.hpp"
 
@@ -133,6 +134,63 @@ int for_each_piece(size_t rows, size_t run, size_t chunk, F&& f) {
         if (const int st = f(Piece{r, 1, off, std::min(chunk, run - off)})) return st;
   }
   return BF_OK;
+}
+
+bf_scatter_op make_op(int kind, int peer, int group, int src_space, size_t src_off, size_t src_pitch, int dst_space,
+                      size_t dst_off, size_t dst_pitch, size_t width, size_t height) {
+  bf_scatter_op o{};
+  o.kind = kind;
+  o.peer = peer;
+  o.group = group;
+  o.src_space = src_space;
+  o.dst_space = dst_space;
+  o.src_off = src_off;
+  o.src_pitch = src_pitch;
+  o.dst_off = dst_off;
+  o.dst_pitch = dst_pitch;
+  o.width = width;
+  o.height = height;
+  return o;
+}
+
+// The operation list of one rank's part of a scatter (bf_scatter_plan): the root 2-D packs every peer's slice of
+// each piece into its staging slot -- peer r at slot r < root ? r : r - 1, N - 1 slots -- and its own rows straight
+// into `slice`, then one RCCL group sends each peer its piece; at one rank the root's own piece is packed and moved by
+// a self send/receive instead.  A peer receives each piece from the root in the same group order, so the k-th send
+// root -> r pairs with r's k-th receive.
+std::vector<bf_scatter_op> scatter_plan(int nranks, int rank, int root, size_t rows, size_t run, size_t chunk,
+                                        size_t* staging_bytes) {
+  std::vector<bf_scatter_op> ops;
+  const size_t pitch = run * static_cast<size_t>(nranks);  // the band's (b, a) row
+  const size_t slice_bytes = run * rows;
+  const bool self_p2p = nranks == 1;
+  const int npeers = self_p2p ? 1 : nranks - 1;
+  *staging_bytes = rank == root ? slice_bytes * static_cast<size_t>(npeers) : 0;
+  auto slot = [&](int r) { return slice_bytes * static_cast<size_t>(self_p2p ? 0 : (r < root ? r : r - 1)); };
+  int group = 0;
+  (void)for_each_piece(rows, run, chunk, [&](const Piece& pc) -> int {
+    const size_t off = pc.row0 * run + pc.off, bytes = pc.nrows * pc.width;
+    if (rank == root) {
+      for (int r = 0; r < nranks; ++r) {
+        const bool direct = r == root && !self_p2p;
+        ops.push_back(make_op(BF_SCATTER_COPY2D, r, group, BF_SPACE_BAND,
+                              pc.row0 * pitch + pc.off + run * static_cast<size_t>(r), pitch,
+                              direct ? BF_SPACE_SLICE : BF_SPACE_STAGING, direct ? off : slot(r) + off, run, pc.width,
+                              pc.nrows));
+      }
+      for (int r = 0; r < nranks; ++r) {
+        if (r == root && !self_p2p) continue;
+        ops.push_back(make_op(BF_SCATTER_SEND, r, group, BF_SPACE_STAGING, slot(r) + off, 0, 0, 0, 0, bytes, 1));
+        if (r == root)
+          ops.push_back(make_op(BF_SCATTER_RECV, root, group, 0, 0, 0, BF_SPACE_SLICE, off, 0, bytes, 1));
+      }
+    } else {
+      ops.push_back(make_op(BF_SCATTER_RECV, root, group, 0, 0, 0, BF_SPACE_SLICE, off, 0, bytes, 1));
+    }
+    ++group;
+    return BF_OK;
+  });
+  return ops;
 }
 }  // namespace
 
@@ -245,6 +303,23 @@ int bf_comm_allreduce_max(bf_comm* c, double* value) {
   return BF_OK;
 }
 
+int bf_scatter_plan(int nranks, int rank, int root, int B, int A, int C, int T, size_t chunk, bf_scatter_op* ops,
+                    size_t capacity, size_t* n_ops, size_t* staging_bytes) {
+  BF_REQUIRE(n_ops != nullptr && staging_bytes != nullptr, "bf_scatter_plan: null pointer");
+  BF_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks && root >= 0 && root < nranks,
+             "bf_scatter_plan: rank %d, root %d of %d ranks", rank, root, nranks);
+  BF_REQUIRE(B > 0 && A > 0 && C > 0 && T > 0, "bf_scatter_plan: bad shape B=%d A=%d C=%d T=%d", B, A, C, T);
+  const size_t run = static_cast<size_t>(C) * T * 4;
+  const auto plan = scatter_plan(nranks, rank, root, static_cast<size_t>(B) * A, run, chunk ? chunk : scatter_chunk(),
+                                 staging_bytes);
+  *n_ops = plan.size();
+  if (ops == nullptr) return BF_OK;
+  BF_REQUIRE(capacity >= plan.size(), "bf_scatter_plan: %zu ops need a capacity of at least that", plan.size());
+  std::copy(plan.begin(), plan.end(), ops);
+  bf::clear_error();
+  return BF_OK;
+}
+
 int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, int A, int C, int T, int root,
                        void* stream) {
   BF_REQUIRE(c != nullptr && slice != nullptr, "bf_channel_scatter: null pointer");
@@ -253,67 +328,53 @@ int bf_channel_scatter(bf_comm* c, const uint8_t* band, uint8_t* slice, int B, i
   BF_REQUIRE(c->rank != root || band != nullptr, "bf_channel_scatter: the root needs the band");
   DeviceGuard dg(c->device);
   hipStream_t st = bf::as_stream(stream);
-  const size_t run = static_cast<size_t>(C) * T * 4;            // one (b, a) channel run of a slice
-  const size_t pitch = run * static_cast<size_t>(c->nranks);    // the band's (b, a) row
-  const size_t rows = static_cast<size_t>(B) * A;
-  const size_t slice_bytes = run * rows;
-  const size_t chunk = scatter_chunk();
-  if (c->rank == root) {
-    // At one rank the root's slice goes through RCCL too (pack, then a self ncclSend/ncclRecv), so the one-GPU box
-    // runs the point-to-point path of N ranks.  At N > 1 the root's own slice is one 2-D copy (no staging round
-    // trip: a deployment never needs it) and only the N - 1 peer slices are packed.
-    const bool self_p2p = c->nranks == 1;
-    const int npeers = self_p2p ? 1 : c->nranks - 1;
-    const size_t need = slice_bytes * static_cast<size_t>(npeers);
-    if (need > c->staging_bytes) {
-      if (c->staging) {
-        BF_HIP(hipEventSynchronize(c->sent));
-        BF_HIP(hipFree(c->staging));
-        c->staging = nullptr;
-        c->staging_bytes = 0;
-      }
-      BF_HIP(hipMalloc(&c->staging, need));
-      c->staging_bytes = need;
+  size_t need = 0;
+  const auto plan = scatter_plan(c->nranks, c->rank, root, static_cast<size_t>(B) * A, static_cast<size_t>(C) * T * 4,
+                                 scatter_chunk(), &need);
+  if (need > c->staging_bytes) {
+    if (c->staging) {
+      BF_HIP(hipEventSynchronize(c->sent));
+      BF_HIP(hipFree(c->staging));
+      c->staging = nullptr;
+      c->staging_bytes = 0;
     }
-    // the previous scatter's sends may still read the staging buffer on another stream
-    BF_HIP(hipStreamWaitEvent(st, c->sent, 0));
-    uint8_t* stg = static_cast<uint8_t*>(c->staging);
-    auto slot = [&](int r) {  // the peer's packed slice in staging
-      return stg + slice_bytes * static_cast<size_t>(self_p2p ? 0 : (r < root ? r : r - 1));
-    };
-    const int st_pieces = for_each_piece(rows, run, chunk, [&](const Piece& pc) -> int {
-      const size_t off = pc.row0 * run + pc.off, bytes = pc.nrows * pc.width;
-      const uint8_t* src = band + pc.row0 * pitch + pc.off;
-      for (int r = 0; r < c->nranks; ++r) {
-        uint8_t* dst = (r == root && !self_p2p) ? slice + off : slot(r) + off;
-        BF_HIP(hipMemcpy2DAsync(dst, run, src + run * static_cast<size_t>(r), pitch, pc.width, pc.nrows,
-                                hipMemcpyDeviceToDevice, st));
-      }
-      BF_RCCL(rccl().group_start());
-      for (int r = 0; r < c->nranks; ++r) {
-        if (r == root && !self_p2p) continue;
-        ncclResult_t e = rccl().send(slot(r) + off, bytes, ncclUint8, r, c->comm, st);
-        if (e == ncclSuccess && r == root) e = rccl().recv(slice + off, bytes, ncclUint8, root, c->comm, st);
-        if (e != ncclSuccess) {
-          (void)rccl().group_end();
-          return rccl_fail(e, r == root ? "ncclSend/ncclRecv (self)" : "ncclSend");
-        }
-      }
-      BF_RCCL(rccl().group_end());
-      return BF_OK;
-    });
-    if (st_pieces != BF_OK) return st_pieces;
-    BF_HIP(hipEventRecord(c->sent, st));
-    c->p2p_sent += slice_bytes * static_cast<unsigned long long>(npeers);
-    if (self_p2p) c->p2p_received += slice_bytes;
-  } else {
-    const int st_pieces = for_each_piece(rows, run, chunk, [&](const Piece& pc) -> int {
-      BF_RCCL(rccl().recv(slice + pc.row0 * run + pc.off, pc.nrows * pc.width, ncclUint8, root, c->comm, st));
-      return BF_OK;
-    });
-    if (st_pieces != BF_OK) return st_pieces;
-    c->p2p_received += slice_bytes;
+    BF_HIP(hipMalloc(&c->staging, need));
+    c->staging_bytes = need;
   }
+  // the previous scatter's sends may still read the staging buffer on another stream
+  if (c->rank == root) BF_HIP(hipStreamWaitEvent(st, c->sent, 0));
+  auto at = [&](int space, unsigned long long off) -> uint8_t* {
+    uint8_t* base = space == BF_SPACE_BAND      ? const_cast<uint8_t*>(band)
+                    : space == BF_SPACE_STAGING ? static_cast<uint8_t*>(c->staging)
+                                                : slice;
+    return base + off;
+  };
+  unsigned long long sent = 0, received = 0;
+  for (size_t i = 0; i < plan.size();) {
+    const int group = plan[i].group;
+    for (; i < plan.size() && plan[i].group == group && plan[i].kind == BF_SCATTER_COPY2D; ++i) {
+      const bf_scatter_op& o = plan[i];
+      BF_HIP(hipMemcpy2DAsync(at(o.dst_space, o.dst_off), o.dst_pitch, at(o.src_space, o.src_off), o.src_pitch, o.width,
+                              o.height, hipMemcpyDeviceToDevice, st));
+    }
+    BF_RCCL(rccl().group_start());
+    for (; i < plan.size() && plan[i].group == group; ++i) {
+      const bf_scatter_op& o = plan[i];
+      const ncclResult_t e =
+          o.kind == BF_SCATTER_SEND ? rccl().send(at(o.src_space, o.src_off), o.width, ncclUint8, o.peer, c->comm, st)
+          : o.kind == BF_SCATTER_RECV ? rccl().recv(at(o.dst_space, o.dst_off), o.width, ncclUint8, o.peer, c->comm, st)
+                                      : ncclInvalidUsage;  // a copy after the group's sends: not a plan this file makes
+      if (e != ncclSuccess) {
+        (void)rccl().group_end();
+        return rccl_fail(e, o.kind == BF_SCATTER_SEND ? "ncclSend" : "ncclRecv");
+      }
+      (o.kind == BF_SCATTER_SEND ? sent : received) += o.width;
+    }
+    BF_RCCL(rccl().group_end());
+  }
+  if (c->rank == root) BF_HIP(hipEventRecord(c->sent, st));
+  c->p2p_sent += sent;
+  c->p2p_received += received;
   BF_HIP(hipEventRecord(c->done, st));
   c->pending = true;
   bf::clear_error();

@@ -56,6 +56,29 @@ def gather_channel_slices(part, group):
     return np.concatenate([np.frombuffer(g, part.dtype).reshape(part.shape) for g in got], axis=2)
 
 
+class ScatterOp(ctypes.Structure):
+    """include/bf.h bf_scatter_op."""
+    _fields_ = [("kind", ctypes.c_int), ("peer", ctypes.c_int), ("group", ctypes.c_int), ("src_space", ctypes.c_int),
+                ("dst_space", ctypes.c_int), ("reserved", ctypes.c_int), ("src_off", ctypes.c_ulonglong),
+                ("src_pitch", ctypes.c_ulonglong), ("dst_off", ctypes.c_ulonglong), ("dst_pitch", ctypes.c_ulonglong),
+                ("width", ctypes.c_ulonglong), ("height", ctypes.c_ulonglong)]
+
+
+SCATTER_COPY2D, SCATTER_SEND, SCATTER_RECV = 1, 2, 3
+SPACE_BAND, SPACE_STAGING, SPACE_SLICE = 1, 2, 3
+
+
+def scatter_plan(nranks, rank, root, B, A, C, T, chunk=0):
+    """libbf's operation list for one rank's part of bf_channel_scatter (bf_scatter_plan: host arithmetic only, the
+    list the scatter executes).  Returns ([op dicts], staging bytes)."""
+    n, staging = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.call("bf_scatter_plan", nranks, rank, root, B, A, C, T, chunk, None, 0, ctypes.byref(n), ctypes.byref(staging))
+    ops = (ScatterOp * max(n.value, 1))()
+    _lib.call("bf_scatter_plan", nranks, rank, root, B, A, C, T, chunk, ops, n.value, ctypes.byref(n),
+              ctypes.byref(staging))
+    return [{f: getattr(o, f) for f, _ in ScatterOp._fields_} for o in ops[:n.value]], staging.value
+
+
 class ChannelScatter:
     """The RCCL channel scatter of libbf (bf_comm_* / bf_channel_scatter).  Rank 0 makes the communicator id and
     `group` (a rendezvous.HostGroup) hands it to every rank; the communicator lives on `context`'s device.

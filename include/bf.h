@@ -33,7 +33,8 @@ extern "C" {
 /* Thread-local message of the last failing call on this thread (replaces GPU_ERRCHK's stderr print). */
 const char* bf_last_error(void);
 /* ABI version: major * 100 + minor.  300: ABI 3.0 -- 0x0500 (BF_FUSED_PATH_WIDE16, accepted by 2.0) is rejected as an
- * unknown path, and bf_coeff_gen_time_study, bf_comm_stats, bf_comm_load and bf_checksum were added. */
+ * unknown path, and bf_coeff_gen_time_study, bf_comm_stats, bf_comm_load and bf_checksum were added.  301: ABI 3.1 --
+ * bf_scatter_plan added (the channel scatter's operation list as a pure host function). */
 int bf_abi_version(void);
 
 /* ---- runtime helpers (device memory, streams, events) -------------------------------------------------
@@ -146,7 +147,8 @@ int bf_beamform(const uint8_t* x, const float* w, float* y, int B, int P, int C,
  * of ABI 2.0, removed from the product in ABI 3.0 (0x0500: the 16-beam float slabs are what WIDE picks for M <= 16; the
  * int8 kernel lives on in the diagnostic build): all three are rejected as unknown.) */
 #define BF_FUSED_ORDER_MASK 0x3000
-#define BF_FUSED_ORDER_CHANNEL 0x1000 /* plain channel-fastest workgroup order */
+#define BF_FUSED_ORDER_CHANNEL 0x1000 /* plain channel-fastest workgroup order (the persistent config-4 float
+                                         kernel walks channel runs and has none: this flag takes the slab kernel) */
 #define BF_FUSED_ORDER_XCD 0x2000     /* XCD-range order (XCD x streams channels [x C/8, (x+1) C/8)) */
 int bf_beamform_fused(const uint8_t* raw, const float* delay_vals, int delay_channels, void* y, int B, int C,
                       int T, int A, int M, int Ctot, int xeng_id, double sample_period, double t0,
@@ -240,6 +242,29 @@ int bf_channel_scatter(bf_comm* comm, const uint8_t* band, uint8_t* slice, int B
                        void* stream);
 int bf_comm_stats(const bf_comm* comm, unsigned long long* sent, unsigned long long* received);
 int bf_comm_load(void);
+
+/* The scatter's plan for one rank: pure host arithmetic (no device, no RCCL), the exact operation list
+ * bf_channel_scatter executes, so the piece / staging-slot / send-receive pairing logic is testable on a CPU for any
+ * N and root (tests/test_multi_rank.py replays the N ranks' plans on host buffers).  Ops in execution order:
+ *   BF_SCATTER_COPY2D: `height` rows of `width` bytes, (src_space, src_off, src_pitch) -> (dst_space, dst_off,
+ *                      dst_pitch); `peer` = the rank whose slice the rows belong to (root only)
+ *   BF_SCATTER_SEND  : `width` bytes at (src_space, src_off) to rank `peer` (ncclSend)
+ *   BF_SCATTER_RECV  : `width` bytes into (dst_space, dst_off) from rank `peer` (ncclRecv)
+ * `group` numbers the pieces: one RCCL group per piece, its COPY2D ops first.  Spaces: the root's band, the root's
+ * staging buffer (`*staging_bytes` long), this rank's slice.  chunk = the piece size in bytes (0: the product's
+ * 256 MiB).  ops == NULL only counts; a capacity below the count fails with BF_ERR_ARG (`*n_ops` holds the count). */
+#define BF_SCATTER_COPY2D 1
+#define BF_SCATTER_SEND 2
+#define BF_SCATTER_RECV 3
+#define BF_SPACE_BAND 1
+#define BF_SPACE_STAGING 2
+#define BF_SPACE_SLICE 3
+typedef struct bf_scatter_op {
+  int kind, peer, group, src_space, dst_space, reserved;
+  unsigned long long src_off, src_pitch, dst_off, dst_pitch, width, height;
+} bf_scatter_op;
+int bf_scatter_plan(int nranks, int rank, int root, int B, int A, int C, int T, size_t chunk, bf_scatter_op* ops,
+                    size_t capacity, size_t* n_ops, size_t* staging_bytes);
 
 /* Position-weighted 64-bit checksum of a 2-D device region (`rows` runs of `run_bytes`, `pitch_bytes` apart; 4-byte
  * words): sum over packed word index i of splitmix64(splitmix64(i) ^ word_i), mod 2^64 -- equal for a packed slice

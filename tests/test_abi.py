@@ -42,7 +42,7 @@ def test_prototypes_match_header():
 
 def test_abi_version_and_error_channel():
     lib = _lib.load()
-    assert lib.bf_abi_version() == 300  # 3.0: WIDE16 (0x500) rejected, four entry points added
+    assert lib.bf_abi_version() == 301  # 3.1: bf_scatter_plan added to 3.0 (WIDE16 (0x500) rejected)
     assert isinstance(_lib.last_error(), str)
 
 

@@ -115,3 +115,68 @@ def test_pmc_mfma_busy():
     assert b["clock_GHz"] == pytest.approx(1.953, abs=1e-3)
     assert bench.pmc_mfma_busy({"FETCH_SIZE": 1.0, "WRITE_SIZE": 1.0}, 1e-3) is None
     assert bench.pmc_mfma_busy("unavailable", 1e-3) is None
+
+
+def test_resolve_world_launch_and_mismatch():
+    """`--gpus N` without a launcher: this process starts the N ranks; under torch.distributed.run --gpus must equal
+    WORLD_SIZE (a mismatch would time a different number of ranks than the command names)."""
+    a = bench.parse(["--gpus", "4"])
+    assert bench.resolve_world(a, env={}) == (4, True)
+    a = bench.parse([])
+    assert bench.resolve_world(a, env={}) == (1, False) and a.gpus == 1
+    a = bench.parse(["--gpus", "1"])
+    assert bench.resolve_world(a, env={}) == (1, False)
+    a = bench.parse(["--gpus", "2"])
+    assert bench.resolve_world(a, env={"WORLD_SIZE": "2"}) == (2, False)
+    a = bench.parse([])
+    assert bench.resolve_world(a, env={"WORLD_SIZE": "8"}) == (8, False) and a.gpus == 8
+    with pytest.raises(ValueError, match="WORLD_SIZE=2"):
+        bench.resolve_world(bench.parse(["--gpus", "8"]), env={"WORLD_SIZE": "2"})
+    with pytest.raises(ValueError, match="WORLD_SIZE=1"):
+        bench.resolve_world(bench.parse(["--gpus", "2"]), env={"WORLD_SIZE": "1"})
+    with pytest.raises(ValueError):
+        bench.resolve_world(bench.parse(["--gpus", "0"]), env={})
+
+
+def _run_bench(args, env_extra=None, timeout=120):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, cwd=ROOT, env=env)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_n_launches_its_own_ranks(n):
+    """`python bench.py --gpus N` with no launcher (the driver's command form) runs N ranks that meet in the TCP
+    rendezvous group: rank 0 reports N ranks, each with its own RANK and LOCAL_RANK (its device)."""
+    import json
+    r = _run_bench(["--gpus", str(n), "--rank-probe"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["gpus_arg"] == n and out["max_rank"] == n - 1
+    assert out["ranks"] == [{"rank": i, "local_rank": i} for i in range(n)]
+    assert out["ranks_launched_by"] == "bench.py"
+
+
+def test_bench_launcher_propagates_a_rank_failure():
+    """A rank that fails (here: no GPU in this container) fails the launch with its status, and the run ends."""
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-secondary"], timeout=180)
+    assert r.returncode != 0
+    assert "exited with status" in r.stderr
+
+
+def test_bench_gpus_mismatch_under_launcher_fails():
+    r = _run_bench(["--gpus", "4", "--rank-probe"], env_extra={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_target_block():
+    # cfg3 f32 beams on the r5 box: 4.295e9 B against a 759.28 us stream -> 0.707: 0.70 is 0.99 of the stream
+    t = bench.target_block(4294983680.0, 759.28)
+    assert t["ceiling_frac"] == pytest.approx(0.7071, abs=1e-4) and t["target_reachable"] is True
+    assert t["target_needs_frac_of_ceiling"] == pytest.approx(0.70 / 0.7071, abs=1e-3)
+    t = bench.target_block(2147483648.0, 428.32)  # a mix whose best stream is below 0.70
+    assert t["target_reachable"] is False and t["target_needs_frac_of_ceiling"] > 1

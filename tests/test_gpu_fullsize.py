@@ -159,6 +159,57 @@ def test_cfg4_shape_matches_oracle(context, command_queue, C, signed):
                           signed=signed)
 
 
+CFG4_WINDOWS = {"first": 0, "middle": 2048 - 32, "last": 4096 - 64}  # 64 channels each; "middle" spans XCD ranges 3|4
+
+
+@pytest.mark.parametrize("path", ["int8", "f32"])
+def test_cfg4_full_size_channel_windows(context, command_queue, path):
+    """Config 4 at its full per-GPU size (C = 4096 of 32768, X-engine 7) through the benched kernels -- int8: the Q14
+    generator + LDS-DMA-ring contraction (w32r); f32: the persistent channel-run kernel (wide_p2) -- with every item
+    of three contiguous 64-channel windows checked against the oracle: the first channels, the middle (across the
+    XCD-range and channel-run boundaries) and the last.  Both kernels are hand-scheduled; round 5's two
+    schedule-dependent wrong-byte bugs hit a few lanes of some items, which 12 sampled items can miss.  int8
+    bit-exact, f32 within the stated tolerance."""
+    A, M, C, T, B, Ctot, xeng = CONFIGS["cfg4"]
+    signed = True
+    raw = random_bytes((B, A, C, T, 2, 2), seed=29, signed=signed)
+    d = delay_model(M, A, seed=31)
+    int8 = path == "int8"
+    out = launch(context, command_queue, "cfg4", raw, d, signed, **(dict(out_int8=True, out_scale=1 / 64) if int8
+                                                                    else {}))
+    for name, c0 in CFG4_WINDOWS.items():
+        sl = np.ascontiguousarray(raw[:, :, c0:c0 + 64])
+        kw = dict(xeng_id=xeng, t0=T0, batch_dt=batch_dt("cfg4"), ch0=C * xeng + c0)
+        if int8:
+            ref = O.fused_beamform_int8(sl, d, Ctot, scale=1 / 64, signed=signed, **kw)
+            np.testing.assert_array_equal(out[:, :, c0:c0 + 64], ref, err_msg=f"window {name} at channel {c0}")
+            assert np.abs(ref.astype(int)).max() >= 8
+        else:
+            ref = O.fused_beamform(sl, d, Ctot, signed=signed, **kw)
+            w = O.fused_tables(d, B, 64, Ctot, A, **kw)
+            assert_beams_allclose(out[:, :, c0:c0 + 64], ref, O.reorder(sl), w, signed=signed)
+
+
+def test_persistent_wide_shape_with_channel_order(context, command_queue):
+    """An explicit channel-fastest workgroup order at the persistent kernel's shape takes the slab kernel (which
+    honours it; the persistent kernel walks channel runs): same contract, whole output within the tolerance."""
+    A, M, C, T, B, Ctot, xeng = 256, 64, 40, 256, 1, 32768, 3
+    raw = random_bytes((B, A, C, T, 2, 2), seed=41, signed=True)
+    d = delay_model(M, A, seed=41)
+    t0, bdt = 2e-3, T * 2 * Ctot * TS
+    op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, sample_period=TS, delay_channels=1,
+                                 sample_signed=True, t0=t0, batch_dt=bdt,
+                                 workgroup_order="channel").instantiate(command_queue)
+    op.ensure_all_bound()
+    op.buffer("inSamples").set(command_queue, raw)
+    op.buffer("delay_vals").set(command_queue, d)
+    op()
+    y = op.buffer("outData").get(command_queue)
+    assert_beams_allclose(y, O.fused_beamform(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, signed=True),
+                          O.reorder(raw), O.fused_tables(d, B, C, Ctot, A, xeng_id=xeng, t0=t0, batch_dt=bdt),
+                          signed=True)
+
+
 @pytest.mark.parametrize("M,C,B,signed,tau_samples", [
     (32, 37, 1, True, 10), (96, 21, 2, False, 10), (64, 300, 1, True, 10), (64, 40, 1, True, 2e5)])
 def test_persistent_wide_kernel_shapes(context, command_queue, M, C, B, signed, tau_samples):

@@ -119,6 +119,29 @@ def test_bench_multi_rank_rehearsal(tmp_path):
     sec = line["secondary"]
     assert [s["workload"][:4] for s in sec] == ["cfg4", "cfg4"], sec
     assert all("error" not in s and s["n_gpus"] == 2 and s["value"] > 0 for s in sec), sec
+    assert line["config"]["ranks_launched_by"].startswith("external")
+
+
+def test_bench_gpus_two_without_launcher(tmp_path):
+    """The driver's own command form, `python bench.py --gpus 2 ...` with no torch.distributed.run: bench.py starts
+    its two ranks itself (both on this one GPU, host scatter backend since RCCL refuses two ranks on one device).
+    Both ranks time their X-engine's shard and the config-4 secondaries; rank 0 prints the one line."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--settle-ms", "0", "--scatter-backend", "host", "--workload", "cfg3", "--nbuf", "1"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["ranks_launched_by"] == "bench.py"
+    assert line["scatter"]["backend"] == "host" and line["scatter"]["ranks"] == 2
+    assert len(line["per_rank_avg_launch_us"]) == 2 and all(t > 0 for t in line["per_rank_avg_launch_us"])
+    sec = line["secondary"]
+    assert [s["workload"][:4] for s in sec] == ["cfg4", "cfg4"], sec
+    for s in sec:
+        assert "error" not in s and s["n_gpus"] == 2 and s["value"] > 0, s
+        assert len(s["per_rank_avg_launch_us"]) == 2 and all(t > 0 for t in s["per_rank_avg_launch_us"]), s
 
 
 def test_bench_rccl_scatter_path_one_rank(tmp_path):

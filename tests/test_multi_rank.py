@@ -262,3 +262,105 @@ def test_scatter_verify_any_root(root, bad_rank):
         else:
             assert [x["rank"] for x in report] == [0, 1, 2]
             assert [x["match"] for x in report] == [r != bad_rank for r in range(world)]
+
+
+def _replay_scatter(N, root, B, A, C, T, chunk):
+    """Replay every rank's bf_scatter_plan (libbf's own operation list for bf_channel_scatter) on host buffers:
+    COPY2D as strided byte copies, each SEND queued on its (root -> peer) link, each RECV taking the next message of
+    its link in order (RCCL point-to-point matching).  Returns (band, per-rank slices, per-rank write counts of the
+    slices, root staging write counts, bytes sent / received per rank)."""
+    from dpdk_dc_sand_amd.shard import (SCATTER_COPY2D, SCATTER_RECV, SCATTER_SEND, SPACE_BAND, SPACE_SLICE,
+                                        SPACE_STAGING, scatter_plan)
+    rng = np.random.default_rng(N * 100 + root)
+    run = C * T * 4
+    slice_bytes = B * A * run
+    band = rng.integers(0, 256, B * A * run * N, dtype=np.uint8)
+    plans = {r: scatter_plan(N, r, root, B, A, C, T, chunk) for r in range(N)}
+    staging = np.zeros(plans[root][1], np.uint8)
+    staging_writes = np.zeros(plans[root][1], np.int32)
+    slices = {r: np.zeros(slice_bytes, np.uint8) for r in range(N)}
+    writes = {r: np.zeros(slice_bytes, np.int32) for r in range(N)}
+    links = {r: [] for r in range(N)}  # root -> r, in send order
+    sent = {r: 0 for r in range(N)}
+    received = {r: 0 for r in range(N)}
+    for r in range(N):
+        assert plans[r][1] == (slice_bytes * (max(N - 1, 1)) if r == root else 0)
+
+    def space(r, s):
+        return {SPACE_BAND: (band, None), SPACE_STAGING: (staging, staging_writes),
+                SPACE_SLICE: (slices[r], writes[r])}[s]
+
+    def run_ops(r, ops):
+        last_group, copies_open = -1, True
+        for o in ops:
+            assert o["group"] >= last_group
+            if o["group"] != last_group:
+                last_group, copies_open = o["group"], True
+            if o["kind"] == SCATTER_COPY2D:
+                assert r == root and copies_open, "a copy after its group's sends"
+                src, _ = space(r, o["src_space"])
+                dst, cnt = space(r, o["dst_space"])
+                for h in range(o["height"]):
+                    s0, d0 = o["src_off"] + h * o["src_pitch"], o["dst_off"] + h * o["dst_pitch"]
+                    dst[d0:d0 + o["width"]] = src[s0:s0 + o["width"]]
+                    cnt[d0:d0 + o["width"]] += 1
+            elif o["kind"] == SCATTER_SEND:
+                copies_open = False
+                assert r == root and o["src_space"] == SPACE_STAGING
+                src, _ = space(r, o["src_space"])
+                links[o["peer"]].append(src[o["src_off"]:o["src_off"] + o["width"]].copy())
+                sent[r] += o["width"]
+            else:
+                assert o["kind"] == SCATTER_RECV and o["peer"] == root and o["dst_space"] == SPACE_SLICE
+                copies_open = False
+                msg = links[r].pop(0)
+                assert len(msg) == o["width"], "a receive paired with a send of another size"
+                dst, cnt = space(r, o["dst_space"])
+                dst[o["dst_off"]:o["dst_off"] + o["width"]] = msg
+                cnt[o["dst_off"]:o["dst_off"] + o["width"]] += 1
+                received[r] += o["width"]
+
+    run_ops(root, plans[root][0])
+    for r in range(N):
+        if r != root:
+            run_ops(r, plans[r][0])
+    assert all(not q for q in links.values()), "sends left without a receive"
+    return band.reshape(B, A, C * N, T * 4), slices, writes, staging_writes, sent, received
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 4])
+@pytest.mark.parametrize("root_at", ["first", "last", "middle"])
+@pytest.mark.parametrize("chunk", [0, 256, 100, 48], ids=["one-piece", "row-blocks", "ragged-blocks", "row-segments"])
+def test_scatter_plan_moves_every_band_byte_once(N, root_at, chunk):
+    """the scatter's piece and staging-slot planning and its send/receive pairing, on CPU.  For N = 1..4
+    ranks, roots first / middle / last, whole-row pieces, ragged row blocks and rows longer than a piece (sub-row
+    segments): every rank's slice equals its channel block [C r, C (r + 1)) of the band, every slice byte and every
+    staging byte is written exactly once, and the byte counts match what bf_comm_stats reports."""
+    root = {"first": 0, "last": N - 1, "middle": N // 2}[root_at]
+    B, A, C, T = 2, 3, 2, 16  # run = 128 bytes, 6 rows
+    band, slices, writes, staging_writes, sent, received = _replay_scatter(N, root, B, A, C, T, chunk)
+    for r in range(N):
+        want = np.ascontiguousarray(band[:, :, C * r:C * (r + 1)]).reshape(-1)
+        np.testing.assert_array_equal(slices[r], want, err_msg=f"rank {r}")
+        assert (writes[r] == 1).all(), f"rank {r}: slice bytes written {np.unique(writes[r])} times"
+        # the root's own slice is one 2-D copy at N > 1 (a self send/receive only at one rank)
+        assert received[r] == (0 if (r == root and N > 1) else want.size)
+    assert (staging_writes == 1).all()
+    assert sent[root] == B * A * C * T * 4 * max(N - 1, 1)
+    assert all(sent[r] == 0 for r in range(N) if r != root)
+
+
+def test_scatter_plan_argument_checks():
+    from dpdk_dc_sand_amd.shard import ScatterOp, scatter_plan
+    with pytest.raises(_lib.BeamformerError, match="root 2 of 2"):
+        scatter_plan(2, 0, 2, 1, 1, 1, 16)
+    with pytest.raises(_lib.BeamformerError, match="bad shape"):
+        scatter_plan(2, 0, 0, 0, 1, 1, 16)
+    n, stg = ctypes.c_size_t(), ctypes.c_size_t()
+    ops = (ScatterOp * 1)()
+    with pytest.raises(_lib.BeamformerError, match="capacity"):
+        _lib.call("bf_scatter_plan", 3, 0, 0, 2, 2, 1, 16, 64, ops, 1, ctypes.byref(n), ctypes.byref(stg))
+    assert n.value > 1
+    # the product piece: a 2 GiB cfg3 slice (8 x 64 rows of 1 MiB) moves in 8 groups of 256 MiB
+    plan, staging = scatter_plan(2, 1, 0, 8, 64, 4096, 256)
+    assert len(plan) == 8 and all(o["width"] == 256 << 20 for o in plan) and staging == 0

@@ -95,3 +95,19 @@ def test_no_inline_asm_result_reaches_an_mfma_unpadded():
     bad = [f"{src}: {fn[:90]}: {a} -> +{n} {m}" for src, asm in isas.items()
            for fn, a, m, n in shc.scan_asm_to_mfma(asm, window=2)]
     assert not bad, "\n".join(bad[:20])
+
+
+def test_store_hazard_scanner_counts_nop_wait_states():
+    """The scanner's window is wait states, not instructions: `s_nop 0` is one state (a VALU right after it still
+    hits a 2-state window), `s_nop 1` two."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import store_hazard_check as shc
+    head = "_Zk:\n  buffer_store_dwordx4 v[80:83], v1, s[0:3], 0 offen\n"
+    assert len(shc.scan(head + "  s_nop 0\n  v_add_u32 v83, v1, v2\n")[1]) == 1
+    assert len(shc.scan(head + "  s_nop 1\n  v_add_u32 v83, v1, v2\n")[1]) == 0
+    assert len(shc.scan(head + "  s_nop 0\n  s_nop 0\n  v_add_u32 v83, v1, v2\n")[1]) == 0
+    assert len(shc.scan(head + "  v_add_u32 v9, v1, v2\n  v_add_u32 v83, v1, v2\n")[1]) == 1
+    assert len(shc.scan(head + "  v_add_u32 v9, v1, v2\n  s_nop 0\n  v_add_u32 v83, v1, v2\n")[1]) == 0
+    assert len(shc.scan(head + "  v_add_u32 v84, v1, v2\n")[1]) == 0
+    assert shc.nop_states("s_nop 0x3") == 4

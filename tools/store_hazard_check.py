@@ -39,22 +39,30 @@ def scan(asm, window=2):
         total += 1
         ops = [x.rstrip(",") for x in t.split()[1:]]
         data = _regs(ops[0] if op.startswith("buffer") else ops[1])
-        for j in range(1, window + 1):
-            if i + j >= len(lines) or lines[i + j][0] != fn:
-                break
+        elapsed, j = 0, 1  # wait states between the store and instruction i + j
+        while elapsed < window and i + j < len(lines) and lines[i + j][0] == fn:
             n = lines[i + j][1]
             nop = n.split()[0]
-            if nop.startswith("s_nop"):
-                break  # s_nop k is k + 1 wait states: enough for this window
+            j += 1
+            if nop == "s_nop":  # s_nop k is k + 1 wait states (s_nop 0: one, not enough for a 2-state window)
+                elapsed += nop_states(n)
+                continue
             if nop.startswith("v_") and not nop.startswith("v_mfma"):
                 parts = [x.rstrip(",") for x in n.split()[1:]]
                 dst = _regs(parts[0]) if parts else set()
                 if "swap" in nop and len(parts) > 1:
                     dst |= _regs(parts[1])
                 if dst & data:
-                    hits.append((fn, t, n, j))
+                    hits.append((fn, t, n, elapsed + 1))
                     break
+            elapsed += 1
     return total, hits
+
+
+def nop_states(line):
+    """Wait states of an `s_nop k` line: k + 1."""
+    parts = line.split()
+    return int(parts[1], 0) + 1 if len(parts) > 1 else 1
 
 
 def scan_asm_to_mfma(asm, window=2):
