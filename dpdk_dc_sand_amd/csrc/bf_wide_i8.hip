@@ -866,7 +866,10 @@ __device__ __forceinline__ i32x4_t w32r_frag_im(const i32x4_t& f) {
 
 // Mode (diagnostics only): 4 no stores, 8 no voltage DMA (the slots' stale bytes), 16 no table loads / expansion,
 // 32 the step's four DMA pieces issued as one burst before its MFMAs (the product spreads them, one per 8 MFMAs),
-// 64 a pass's four beam stores back to back after its requantisation.
+// 64 a pass's four beam stores back to back after its requantisation; 128 the DMA pieces issued through a
+// zero-record descriptor (the instructions and waits stay, no bytes move: their issue cost alone), 256 the same for
+// the beam stores; 512 the four pieces of a step at one M0 (the LDS offset in the instruction's immediate, the
+// global offset compensated in soffset).
 template <bool Pow2, int Mode = 0>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(FusedArgs P) {
   constexpr int Sp = 8, NP = 2, kCh = kW32RChannels;
@@ -891,8 +894,8 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
   const uint32_t ant_stride = static_cast<uint32_t>(C) * static_cast<uint32_t>(P.T) * 4u;  // host: A C T 4 < 2^31
   const uint32_t ch_bytes = static_cast<uint32_t>(P.T) * 4u;
   const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * C + c0) * static_cast<size_t>(P.T) * 4;
-  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0x7fffffff,
-                                                                        0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(base), 0, (Mode & 128) ? 0 : 0x7fffffff, 0x00020000);
   const uint32_t dma_voff = static_cast<uint32_t>(8 * ((lane >> 3) & 3) + (lane >> 5)) * ant_stride +
                             16u * static_cast<uint32_t>(lane & 7);
   int4* const slot0 = w32r_slot0 + 256 * wave;
@@ -909,9 +912,19 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
                                           static_cast<uint32_t>(wave + 4 * lp) * 128u);
   };
   auto dma_piece = [&](int4* slot, int k, uint32_t sb) {
-    if constexpr ((Mode & 8) == 0)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lds_void_ptr)(slot + 64 * k), 16, dma_voff,
-                                               sb + 2u * static_cast<uint32_t>(k) * ant_stride, 0, 0);
+    if constexpr ((Mode & 8) == 0) {
+      if constexpr ((Mode & 512) != 0) {
+        const uint32_t so = sb + 2u * static_cast<uint32_t>(k) * ant_stride - 1024u * k;
+        switch (k) {  // (the immediate must be a constant: k is one after unrolling)
+#define BF_W32R_DMA(K) \
+  case K: __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lds_void_ptr)slot, 16, dma_voff, so, 1024 * K, 0); break;
+          BF_W32R_DMA(0) BF_W32R_DMA(1) BF_W32R_DMA(2) BF_W32R_DMA(3)
+#undef BF_W32R_DMA
+        }
+      } else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lds_void_ptr)(slot + 64 * k), 16, dma_voff,
+                                                 sb + 2u * static_cast<uint32_t>(k) * ant_stride, 0, 0);
+    }
   };
   auto advance = [&]() {
     ++issued;
@@ -979,7 +992,8 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
 
   const float s32 = P.out_scale * 0x1p-14f;
   const int M2 = 2 * P.M;
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(P.y, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(P.y, 0, (Mode & 256) ? 0 : 0x7fffffff,
+                                                                        0x00020000);
   // the lane's part of a beam-row store offset (sample 2 tl + i of the wave's 32, row piece of lane group h)
   const uint32_t so_lane = static_cast<uint32_t>(2 * tl * M2 + 16 * (h >> 1) + 32 * (h & 1));
   for (int kc = 0; kc < nk; ++kc) {
@@ -1133,6 +1147,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
 
 #ifdef BF_DIAG
 #include "diag/wide_i8_w32h.inc"  // round 4's halved-image kernel (diagnostic build only)
+#include "diag/wide_i8_w32r3.inc"  // round 6's three-slot ring (measured slower; diagnostic build only)
 #endif
 
 template <bool Signed, int Mode>
