@@ -182,6 +182,7 @@ __global__ __launch_bounds__(kThreads) void beamform_table_ring_kernel(const uin
                                                                        float* __restrict__ y, int NB, int A, int M,
                                                                        int S, int NT, int nslabs, long long nbpc,
                                                                        int xcd) {
+  static_assert(kDiagBuild || Mode == 0, "diagnostic Mode bits in a product instantiation");
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int slab;
@@ -339,6 +340,7 @@ template <bool Signed, int NTS, int R, int UPT, int Mode = 0, int G = 2>
 __global__ __launch_bounds__(kThreads, 2) void beamform_table_persist_kernel(
     const uint8_t* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int NB, int A, int M, int S,
     int NT, int nslabs, long long nbpc, int xcd, long long nitems) {
+  static_assert(kDiagBuild || Mode == 0, "diagnostic Mode bits in a product instantiation");
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
@@ -544,6 +546,7 @@ template <bool Signed, int Mode, int NW, int Occ = NW / 2>
 __global__ __launch_bounds__(NW * 64, Occ) void beamform_table_os_kernel(const uint8_t* __restrict__ x,
                                                                       const float* __restrict__ w,
                                                                       float* __restrict__ y, int A) {
+  static_assert(kDiagBuild || Mode == 0, "diagnostic Mode bits in a product instantiation");
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   constexpr int NTL = kOsCols / 16, RG = 16 / NW, M2 = kOsCols, T = kOsRows;
   constexpr int CPT = 16 / NW;            // table columns per thread

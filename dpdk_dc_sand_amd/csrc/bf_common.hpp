@@ -60,6 +60,14 @@ inline const char* diag_env(const char* name) {
 #endif
 }
 
+// The kernels' compile-time `Mode` ablation bits (skip a phase, stamp, re-route a stream) exist for the diagnostic
+// build only: a product instantiation carrying one fails to compile (static_assert(kDiagBuild || ...) per kernel).
+#ifdef BF_DIAG
+constexpr bool kDiagBuild = true;
+#else
+constexpr bool kDiagBuild = false;
+#endif
+
 constexpr int kSamplesPerBlock = 16;  // matrix_multiply.py:76 (128 // 8)
 
 // Launch flags of bf_beamform_fused* and bf_pipeline_create (include/bf.h): only known bits, a defined kernel

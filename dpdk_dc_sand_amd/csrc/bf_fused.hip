@@ -310,6 +310,7 @@ __device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, in
 // add are one exact FMA (as requant_bits<true>).
 template <bool Signed, bool OutI8, int NTS, bool Exact, bool Full, int Mode = 0, int Occ = 1, bool Pow2 = false>
 __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_item_kernel(FusedArgs P) {
+  static_assert(kDiagBuild || (Mode & (kSkipCoef | kSkipMfma | kSkipStore | kSkipLoad)) == 0, "diagnostic Mode bits in a product instantiation");
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
@@ -882,6 +883,7 @@ __device__ void store_f32acc_i8_rows(const FusedArgs& P, int b, int c, int p, in
 // Pow2: out_scale * 2^-14 is a power of two (requant_bits<true>: one exact FMA).
 template <bool Signed, int NTS, bool Full, int Mode = 0, int Occ = 3, bool A64 = false, bool Pow2 = false>
 __global__ __launch_bounds__(kThreads, Occ) void beamform_fused_i8_item_kernel(FusedArgs P) {
+  static_assert(kDiagBuild || (Mode & (kSkipCoef | kSkipMfma | kSkipStore | kSkipLoad)) == 0, "diagnostic Mode bits in a product instantiation");
   extern __shared__ __attribute__((aligned(16))) half8 lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;

@@ -236,6 +236,7 @@ __device__ __forceinline__ void w32_mfma_pf(const int4* __restrict__ fr, int s, 
 // without the phasor math, 256 the phasor math on register-made delays (no model loads).
 template <bool Signed, int Mode = 0, bool Gain = false>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32_kernel(FusedArgs P) {
+  static_assert(kDiagBuild || Mode == 0, "diagnostic Mode bits in a product instantiation");
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
   // Mode 128 (diagnostics): per-wave s_memtime cycles of the phases -> P.gain as uint64 [wave][4]: coefficient
   // phase (to the barrier), contraction loops, requantise + stores, total
@@ -541,6 +542,7 @@ constexpr int kW32TChannels = 4;
 template <bool Signed, int Mode = 0, bool Early = true, int kSp = 0, int kNP = 0, int kNB = 4, int kCh = kW32TChannels,
           bool BufLd = false, bool Pow2 = false>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32t_kernel(FusedArgs P) {
+  static_assert(kDiagBuild || Mode == 0, "diagnostic Mode bits in a product instantiation");
   extern __shared__ __attribute__((aligned(16))) int4 lds4[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 4, tl = lane & 15;
@@ -869,9 +871,11 @@ __device__ __forceinline__ i32x4_t w32r_frag_im(const i32x4_t& f) {
 // 64 a pass's four beam stores back to back after its requantisation; 128 the DMA pieces issued through a
 // zero-record descriptor (the instructions and waits stay, no bytes move: their issue cost alone), 256 the same for
 // the beam stores; 512 the four pieces of a step at one M0 (the LDS offset in the instruction's immediate, the
-// global offset compensated in soffset).
+// global offset compensated in soffset); 1024 every channel's voltages from the workgroup's first channel (L2
+// hits after the first), 2048 every beam store into one of 256 8 KiB blocks (L2-resident writes).
 template <bool Pow2, int Mode = 0>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(FusedArgs P) {
+  static_assert(kDiagBuild || Mode == 0, "diagnostic Mode bits in a product instantiation");
   constexpr int Sp = 8, NP = 2, kCh = kW32RChannels;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -908,7 +912,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
   auto dma_sb = [&]() {
     // (readfirstlane: a loop-carried part of it landed in a VGPR, and the DMA's soffset then became a waterfall loop)
     return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(w8_step_base(ls, P.A)) * ant_stride +
-                                          static_cast<uint32_t>(lk) * ch_bytes +
+                                          static_cast<uint32_t>((Mode & 1024) ? 0 : lk) * ch_bytes +
                                           static_cast<uint32_t>(wave + 4 * lp) * 128u);
   };
   auto dma_piece = [&](int4* slot, int k, uint32_t sb) {
@@ -1111,6 +1115,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
             sd[p][i] = u32x4_t{sw0[0], sw1[0], sw0[1], sw1[1]};
             soff[p][i] = (prow + static_cast<uint32_t>(2 * (wave + 4 * pass) * 16 + i)) * static_cast<uint32_t>(M2) +
                          static_cast<uint32_t>(2 * m0);
+            if constexpr ((Mode & 2048) != 0) soff[p][i] = static_cast<uint32_t>(blockIdx.x & 255) * 8192u;
             if constexpr ((Mode & 64) == 0) {
               __builtin_amdgcn_raw_buffer_store_b128(sd[p][i], yrs, so_lane, soff[p][i], 0);
               // Two wait states before any VALU may rewrite the store's data VGPRs: hipcc scheduled a write of its

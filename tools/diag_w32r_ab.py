@@ -4,8 +4,9 @@ check of every variant that must produce the product's beams.
 
     python tools/diag_w32r_ab.py [rounds] [mode ...]
 
-Modes: 2000 + w32r's Mode bits, 3000 + w32r3's (the three-slot ring).  Mode bits (bf_wide_i8.hip): 4 no stores, 8 no voltage DMA, 16 no table, 128 DMA through a zero-record descriptor (the
-instructions issue, no bytes move), 256 the stores likewise, 512 one M0 per step's four DMA pieces."""
+Modes: 2000 (or 10000) + w32r's Mode bits, 3000 + w32r3's (the three-slot ring).  Mode bits (bf_wide_i8.hip): 4 no stores, 8 no voltage DMA, 16 no table, 128 DMA through a zero-record descriptor (the
+instructions issue, no bytes move), 256 the stores likewise, 512 one M0 per step's four DMA pieces, 1024 every channel's voltages from the workgroup's first
+channel (L2 hits), 2048 every store into one of 256 8 KiB blocks (L2-resident writes)."""
 import ctypes
 import os
 import sys
