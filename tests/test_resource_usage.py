@@ -111,3 +111,39 @@ def test_store_hazard_scanner_counts_nop_wait_states():
     assert len(shc.scan(head + "  v_add_u32 v9, v1, v2\n  s_nop 0\n  v_add_u32 v83, v1, v2\n")[1]) == 0
     assert len(shc.scan(head + "  v_add_u32 v84, v1, v2\n")[1]) == 0
     assert shc.nop_states("s_nop 0x3") == 4
+
+
+def test_lds_dma_ring_slot_reads_wait_for_their_dma():
+    """the config-4 int8 kernel's voltage ring (w32r) relies on hipcc's vmcnt bookkeeping for its LDS-DMA
+    slots.  Replaying the vector-memory queue of its main loop in issue order (tools/store_hazard_check.py
+    scan_lds_dma_ring), every slot read finds at most the next step's 4 DMA pieces outstanding -- the DMA that wrote
+    the slot being read has retired -- in both instances."""
+    import re
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import store_hazard_check as shc
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    asm = shc.compile_isa(os.path.join(CSRC, "bf_wide_i8.hip"))
+    kernels = sorted(set(re.findall(r"^(_Z\w*beamform_fused_i8_w32r_kernel\w*):", asm, flags=re.M)))
+    assert len(kernels) == 2, kernels
+    for k in kernels:
+        checked, bad = shc.scan_lds_dma_ring(asm, k, depth=2)
+        assert checked == 64, (k, checked)  # 16 steps x 4 two-row reads per channel
+        assert not bad, (k, bad[:8])
+
+
+def test_lds_dma_ring_check_flags_an_early_read():
+    """The replay itself: a slot read issued while its own DMA is still counted is flagged; after the right
+    s_waitcnt it is not."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import store_hazard_check as shc
+    body = ["_Zk:", ".LBB0_1:",
+            "buffer_load_dwordx4 v1, s[0:3], s4 offen lds"] * 1 + \
+        ["buffer_load_dwordx4 v1, s[0:3], s4 offen lds"] * 3 + \
+        ["{wait}", "ds_read2st64_b64 v[2:5], v6 offset1:1", "s_cbranch_scc1 .LBB0_1", ".Lfunc_end0:"]
+    early = "\n".join(body).replace("{wait}", "s_waitcnt vmcnt(8)")
+    ok = "\n".join(body).replace("{wait}", "s_waitcnt vmcnt(4)")
+    assert shc.scan_lds_dma_ring(early, "_Zk", depth=2)[1]
+    assert shc.scan_lds_dma_ring(ok, "_Zk", depth=2) == (1, [])

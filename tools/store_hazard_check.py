@@ -110,6 +110,56 @@ def scan_asm_to_mfma(asm, window=2):
     return out
 
 
+def scan_lds_dma_ring(asm, kernel, slot_reads=("ds_read2st64_b64", "ds_read_b64", "ds_read2_b64"), pieces=4,
+                      depth=2):
+    """the LDS-DMA voltage ring relies on hipcc's vmcnt bookkeeping (its slots are distinct __shared__
+    objects).  Replays the vector-memory queue of `kernel`'s main loop (the longest backward branch's body, twice,
+    entered with a full ring of `depth` steps x `pieces` DMA pieces in flight): every `s_waitcnt vmcnt(N)` retires the
+    oldest entries down to N, in issue order, as the hardware does.  At each slot read at most (depth - 1) x pieces
+    DMA pieces may still be outstanding (only the next step's), else the read could see a slot its DMA has not
+    written.  Returns (slot reads checked, [(instruction index, DMA pieces outstanding)])."""
+    lines, start = [], None
+    for line in asm.splitlines():
+        t = line.strip()
+        if re.match(r"^" + re.escape(kernel) + r":", t):
+            start = True
+            continue
+        if start is None:
+            continue
+        if t.startswith(".Lfunc_end"):
+            break
+        if not t or t.startswith(";") or (t.startswith(".") and not t.endswith(":")):
+            continue
+        lines.append(t.split(";")[0].strip())
+    labels = {t[:-1]: i for i, t in enumerate(lines) if re.match(r"^\.LBB\w+:$", t)}
+    loops = []
+    for i, t in enumerate(lines):
+        m = re.search(r"s_(?:cbranch_\w+|branch)\s+(\.LBB\w+)", t)
+        if m and labels.get(m.group(1), i + 1) < i:
+            loops.append((i - labels[m.group(1)], labels[m.group(1)], i))
+    if not loops:
+        return 0, []
+    _, head, tail = max(loops)
+    body = [t for t in lines[head + 1:tail + 1] if not t.endswith(":")]
+    queue = ["dma"] * (pieces * depth)
+    checked, bad = 0, []
+    for rep in range(2):
+        for i, t in enumerate(body):
+            op = t.split()[0]
+            if op.startswith(("buffer_", "global_")) and ("load" in op or "store" in op or "atomic" in op):
+                queue.append("dma" if t.endswith(" lds") or " lds " in t else "mem")
+            elif op == "s_waitcnt":
+                m = re.search(r"vmcnt\((\d+)\)", t)
+                if m:
+                    del queue[:max(0, len(queue) - int(m.group(1)))]
+            elif op in slot_reads:
+                n = queue.count("dma")
+                checked += rep
+                if rep and n > (depth - 1) * pieces:
+                    bad.append((i, n))
+    return checked, bad
+
+
 def compile_isa(src, flags=()):
     r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-x", "hip", "-S",
                         "--cuda-device-only", src, "-o", "-"] + list(flags), capture_output=True, text=True,
