@@ -51,8 +51,11 @@ __device__ __forceinline__ bool w32_slot_antenna(int sa, int A, int* a) {
   return *a >= 32 * st && *a < A;
 }
 
-template <bool Gain>
+// Mode (diagnostics only): 1 the unit-gain walk without its stores (one store per thread if a sum is impossible),
+// 2 the stores without the walk (each word its channel index).
+template <bool Gain, int Mode = 0>
 __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
+  static_assert(kDiagBuild || Mode == 0, "diagnostic Mode bits in a product instantiation");
   const int b = blockIdx.z;
   const int c0 = blockIdx.y * P.run;
   const int w = blockIdx.x * 256 + threadIdx.x;  // word within a (b, c[, slab]) block
@@ -120,31 +123,63 @@ __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
   }
   // The undecided channels (~1e-5 of the values, or all of them beyond the guard's range) are only flagged in the
   // walk and re-evaluated exactly after it: no divergent branch inside the recurrence loop (same speed as the
-  // in-walk form, 68.3 vs 67.3 us same process, profiles/r4_o_generator_fixup_ab.txt).
-  unsigned long long fix = 0;  // bit j: channel c0 + j needs the exact evaluation (nrun <= 64)
-  uint32_t* oj = o;
-  for (int j = 0; j < nrun; ++j, oj += words) {
+  // in-walk form, 68.3 vs 67.3 us same process, profiles/r4_o_generator_fixup_ab.txt).  Round 6: the walk is the
+  // generator's cost (without its stores 59.9 of 65.6 us; the stores alone 38.9, profiles/r6_f_*), so per channel:
+  // the flag is wave-wide (a ballot into a scalar mask, no 64-bit VALU shifts; every lane of a flagged channel is
+  // re-evaluated exactly, which rewrites the decided lanes' words with the same contract values), the unit-gain
+  // decision rounds by the float64 magic number (t + 1.5 * 2^52 holds rne(t) in its low word: no float64 -> int
+  // conversion), the word is one v_perm, and the stores go through a buffer resource with the channel's offset in
+  // the scalar soffset (no per-lane 64-bit address update).
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      P.out + (base - static_cast<size_t>(w)), 0, 0x7fffffff, 0x00020000);
+  const uint32_t lane_off = static_cast<uint32_t>(w) * 4u;
+  const uint32_t ch_off = static_cast<uint32_t>(words) * 4u;  // bytes per channel block
+  auto put = [&](int j, uint32_t word) {
+    __builtin_amdgcn_raw_buffer_store_b32(word, ors, lane_off, static_cast<uint32_t>(j) * ch_off, 0);
+  };
+  auto pack = [](int wc, int ws) {  // (Wc & 0xffff) | Ws << 16
+    return __builtin_amdgcn_perm(static_cast<uint32_t>(ws), static_cast<uint32_t>(wc), 0x05040100u);
+  };
+  if constexpr (Mode == 2) {
+    for (int j = 0; j < nrun; ++j) put(j, static_cast<uint32_t>(j));
+    return;
+  }
+  unsigned long long fix = 0;  // wave-uniform: bit j set when some lane left channel c0 + j undecided (nrun <= 64)
+  uint32_t acc = 0;
+  constexpr double kMagic = 0x1.8p52;
+  for (int j = 0; j < nrun; ++j) {
     bool ok = in_range;
-    int wc, ws;
+    uint32_t word;
     if (Gain || !P.unit_fast) {  // (uniform)
-      wc = q14_pair(re * 0x1p-14, gq, &ok);
-      ws = q14_pair(im * 0x1p-14, gq, &ok);
+      word = pack(q14_pair(re * 0x1p-14, gq, &ok), q14_pair(im * 0x1p-14, gq, &ok));
     } else {
-      wc = q14_pair_unit_scaled(re, &ok);
-      ws = q14_pair_unit_scaled(im, &ok);
+      // t = 2^14 v: Q = rne(t) wherever t is farther than the margin from a half-integer (q14_pair_unit_scaled)
+      const double mc = re + kMagic, ms = im + kMagic;
+      int wc = static_cast<int>(static_cast<uint32_t>(__builtin_bit_cast(unsigned long long, mc)));
+      int ws = static_cast<int>(static_cast<uint32_t>(__builtin_bit_cast(unsigned long long, ms)));
+      if (!(fabs(re - (mc - kMagic)) < kQ14UnitMargin)) wc = q14_pair(re * 0x1p-14, 16384.0f, &ok);
+      if (!(fabs(im - (ms - kMagic)) < kQ14UnitMargin)) ws = q14_pair(im * 0x1p-14, 16384.0f, &ok);
+      word = pack(wc, ws);
     }
-    fix |= static_cast<unsigned long long>(!ok) << j;
-    *oj = (static_cast<uint32_t>(wc) & 0xffffu) | (static_cast<uint32_t>(ws) << 16);
+    if (__builtin_amdgcn_ballot_w64(ok) != __builtin_amdgcn_read_exec()) fix |= 1ull << j;
+    if constexpr (Mode == 1)
+      acc += word;
+    else
+      put(j, word);
     const double r2 = fma(re, cd, -im * sd);
     im = fma(re, sd, im * cd);
     re = r2;
   }
-  while (fix) {  // (the same lane rewrites its own word: program order makes the exact value the final one)
+  if constexpr (Mode == 1) {
+    if (acc == 0x9e3779b9u) *o = acc;
+    return;
+  }
+  while (fix) {  // (each lane rewrites its own word: program order makes the exact value the final one)
     const int j = __builtin_ctzll(fix);
     fix &= fix - 1;
     int wc, ws;
     q14_exact(d, static_cast<double>(P.base_ch + c0 + j), P.ctot, P.ts, dt, P.gain, g, &wc, &ws);
-    o[static_cast<size_t>(j) * words] = (static_cast<uint32_t>(wc) & 0xffffu) | (static_cast<uint32_t>(ws) << 16);
+    put(j, pack(wc, ws));
   }
 }
 
@@ -195,6 +230,18 @@ int launch_q14_table(const FusedArgs& P, uint32_t* out, int layout, hipStream_t 
   BF_REQUIRE(layout != kLayoutW32H, "q14 table: the halved-image layout is in the diagnostic build only");
 #endif
   Q.run = std::min(Q.run, 64);  // (the deferred-fixup mask of q14_table_kernel holds 64 channels)
+#ifdef BF_DIAG
+  const char* gm = diag_env("BF_Q14_MODE");
+  if (gm && (atoi(gm) == 1 || atoi(gm) == 2)) {  // measurement: the walk without stores (1) / stores only (2)
+    const long long gx0 = (words + 255) / 256, gy0 = (Q.Cn + Q.run - 1) / Q.run;
+    const dim3 grid(static_cast<unsigned>(gx0), static_cast<unsigned>(gy0), P.B);
+    if (atoi(gm) == 1)
+      hipLaunchKernelGGL((q14_table_kernel<false, 1>), grid, dim3(256), 0, st, Q);
+    else
+      hipLaunchKernelGGL((q14_table_kernel<false, 2>), grid, dim3(256), 0, st, Q);
+    BF_LAUNCHED("q14_table_kernel");
+  }
+#endif
   const long long gx = (words + 255) / 256, gy = (Q.Cn + Q.run - 1) / Q.run;
   BF_REQUIRE(gx < (1LL << 31) && gy < 65536 && P.B < 65536, "q14 table: grid too large");
   if (P.gain)

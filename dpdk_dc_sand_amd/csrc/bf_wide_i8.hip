@@ -1153,6 +1153,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
 #ifdef BF_DIAG
 #include "diag/wide_i8_w32h.inc"  // round 4's halved-image kernel (diagnostic build only)
 #include "diag/wide_i8_w32r3.inc"  // round 6's three-slot ring (measured slower; diagnostic build only)
+#include "diag/wide_i8_w32s.inc"  // round 6's loader-wave form (measured slower; diagnostic build only)
 #endif
 
 template <bool Signed, int Mode>

@@ -1,7 +1,8 @@
 """GPU box: same-process A/B of one fused launch across several builds of libbf.so (e.g. an earlier round's tree
 built under build/ab_<tag>/): the same device buffers, interleaved rounds, median per library; the int8 outputs of
 every library are compared with the first one's (bitwise).
-(AB_DELAYS=ops: the ops benchmark's delay model.)
+(AB_DELAYS=ops: the ops benchmark's delay model.  AB_WS=1: through bf_beamform_fused_ws with a workspace, as the
+operator runs it -- config 4's int8 path is then the Q14 generator + the table-driven contraction.)
 usage: python tools/ab_libs.py <workload cfg3|cfg4> <flags> <scale> <tag=path/to/libbf.so> ..."""
 import ctypes
 import os
@@ -23,6 +24,12 @@ for spec in sys.argv[4:]:
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 7 + \
                  [ctypes.c_double] * 3 + [ctypes.c_int, ctypes.c_float, ctypes.c_void_p]
+    g = lib.bf_beamform_fused_ws
+    g.restype = ctypes.c_int
+    g.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + \
+                 [ctypes.c_int] * 7 + [ctypes.c_double] * 3 + [ctypes.c_int, ctypes.c_float, ctypes.c_void_p,
+                                                               ctypes.c_size_t, ctypes.c_void_p]
+    lib.bf_fused_workspace_bytes.argtypes = [ctypes.c_int] * 6 + [ctypes.POINTER(ctypes.c_size_t)]
     lib.bf_last_error.restype = ctypes.c_char_p
     libs.append((tag, lib))
 B, C, T, A, M, Ctot = SHAPES[wl]
@@ -51,9 +58,20 @@ dv.set(q, d.reshape(-1))
 bdt = T * 2 * Ctot * ts
 
 
+USE_WS = os.environ.get("AB_WS") == "1"
+wsb = ctypes.c_size_t(0)
+if USE_WS:
+    libs[0][1].bf_fused_workspace_bytes(B, C, T, A, M, flags, ctypes.byref(wsb))
+ws = accel.DeviceArray(ctx, (max(wsb.value, 16),), np.uint8)
+
+
 def launch(lib, i):
-    st = lib.bf_beamform_fused(xs[i % 2].ptr, dv.ptr, 1, ys[i % 2].ptr, B, C, T, A, M, Ctot, 0, ts, T0, bdt, flags,
-                               scale, q.handle)
+    if USE_WS:
+        st = lib.bf_beamform_fused_ws(xs[i % 2].ptr, dv.ptr, 1, None, ys[i % 2].ptr, B, C, T, A, M, Ctot, 0, ts, T0,
+                                      bdt, flags, scale, ws.ptr, wsb.value, q.handle)
+    else:
+        st = lib.bf_beamform_fused(xs[i % 2].ptr, dv.ptr, 1, ys[i % 2].ptr, B, C, T, A, M, Ctot, 0, ts, T0, bdt,
+                                   flags, scale, q.handle)
     if st != 0:
         raise RuntimeError(lib.bf_last_error().decode())
 

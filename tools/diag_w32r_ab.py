@@ -4,7 +4,7 @@ check of every variant that must produce the product's beams.
 
     python tools/diag_w32r_ab.py [rounds] [mode ...]
 
-Modes: 2000 (or 10000) + w32r's Mode bits, 3000 + w32r3's (the three-slot ring).  Mode bits (bf_wide_i8.hip): 4 no stores, 8 no voltage DMA, 16 no table, 128 DMA through a zero-record descriptor (the
+Modes: 2000 (or 10000) + w32r's Mode bits, 3000 + w32r3's (the three-slot ring), 4000 + w32s's (loader waves).  Mode bits (bf_wide_i8.hip): 4 no stores, 8 no voltage DMA, 16 no table, 128 DMA through a zero-record descriptor (the
 instructions issue, no bytes move), 256 the stores likewise, 512 one M0 per step's four DMA pieces, 1024 every channel's voltages from the workgroup's first
 channel (L2 hits), 2048 every store into one of 256 8 KiB blocks (L2-resident writes)."""
 import ctypes
@@ -39,7 +39,7 @@ dv = accel.DeviceArray(ctx, (M * A * 4,), np.float32)
 dv.set(q, d.reshape(-1))
 tb = accel.DeviceArray(ctx, (B * C * (M // 32) * 1024 * 8 + 4096,), np.uint32)
 
-EXACT = {2000, 2512, 3000}  # modes that must give the product's beams bitwise (w32r, M0-once w32r, w32r3)
+EXACT = {2000, 2512, 3000, 4000}  # modes that must give the product's beams bitwise (w32r, M0-once w32r, w32r3)
 
 
 def launch(mode, i):
