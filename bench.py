@@ -104,6 +104,7 @@ def parse(argv=None):
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--prof-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--rank-probe", action="store_true", help=argparse.SUPPRESS)  # CPU test of the rank launch
+    p.add_argument("--probe-sleep", type=float, default=0.0, help=argparse.SUPPRESS)
     a = p.parse_args(argv)
     if a.out_f32:
         a.output = "f32"
@@ -157,12 +158,31 @@ def launch_ranks(n, argv, poll_s=0.05, grace_s=20.0):
     (utilities/pcie_bandwidth_tests/main.cpp:214-224), each rank X-engine `rank` (coeff_generator.py:53).  This
     process never touches the GPU; the children inherit stdout, so rank 0's JSON line is the run's output.  If a rank
     fails, the others are stopped (they would wait in a collective) and its exit status is returned."""
+    import signal
     port = free_port_pair()
+
+    def die_with_parent():  # a rank must not outlive this process (a killed launcher would leave GPUs busy)
+        try:
+            import ctypes
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BF_BENCH_LAUNCHER="bench.py")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env, cwd=ROOT))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env, cwd=ROOT,
+                                      preexec_fn=die_with_parent))
+
+    def forward(signum, _frame):  # SIGTERM / SIGINT to the launcher: stop the ranks, then exit with the signal
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
     rc = 0
     try:
         pending = list(range(n))
@@ -832,11 +852,12 @@ def main():
     if args.rank_probe:  # the ranks' rendezvous and timing-bracket collectives only, no GPU (tests/test_bench_logic.py)
         dist.barrier()
         top = dist.max(float(dist.rank))
-        got = dist.group.gather_json({"rank": dist.rank, "local_rank": dist.local_rank}) if dist.group else \
-            [{"rank": 0, "local_rank": 0}]
+        got = dist.group.gather_json({"rank": dist.rank, "local_rank": dist.local_rank, "pid": os.getpid()}) \
+            if dist.group else [{"rank": 0, "local_rank": 0, "pid": os.getpid()}]
         if dist.rank == 0:
             print(json.dumps({"n_gpus": dist.world, "gpus_arg": args.gpus, "max_rank": top, "ranks": got,
                               "ranks_launched_by": os.environ.get("BF_BENCH_LAUNCHER")}), flush=True)
+        time.sleep(args.probe_sleep)
         dist.close()
         return
     from dpdk_dc_sand_amd import accel

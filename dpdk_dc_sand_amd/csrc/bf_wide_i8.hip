@@ -872,7 +872,8 @@ __device__ __forceinline__ i32x4_t w32r_frag_im(const i32x4_t& f) {
 // zero-record descriptor (the instructions and waits stay, no bytes move: their issue cost alone), 256 the same for
 // the beam stores; 512 the four pieces of a step at one M0 (the LDS offset in the instruction's immediate, the
 // global offset compensated in soffset); 1024 every channel's voltages from the workgroup's first channel (L2
-// hits after the first), 2048 every beam store into one of 256 8 KiB blocks (L2-resident writes).
+// hits after the first), 2048 every beam store into one of 256 8 KiB blocks (L2-resident writes), 4096 the second
+// slab's voltage DMA through a zero-record descriptor (one slab's bytes through the CU path: wrong beams for it).
 template <bool Pow2, int Mode = 0>
 __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(FusedArgs P) {
   static_assert(kDiagBuild || Mode == 0, "diagnostic Mode bits in a product instantiation");
@@ -899,7 +900,7 @@ __global__ __launch_bounds__(kW8Threads, 2) void beamform_fused_i8_w32r_kernel(F
   const uint32_t ch_bytes = static_cast<uint32_t>(P.T) * 4u;
   const uint8_t* base = P.raw + (static_cast<size_t>(b) * P.A * C + c0) * static_cast<size_t>(P.T) * 4;
   const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(base), 0, (Mode & 128) ? 0 : 0x7fffffff, 0x00020000);
+      const_cast<uint8_t*>(base), 0, ((Mode & 128) || ((Mode & 4096) && slab == 1)) ? 0 : 0x7fffffff, 0x00020000);
   const uint32_t dma_voff = static_cast<uint32_t>(8 * ((lane >> 3) & 3) + (lane >> 5)) * ant_stride +
                             16u * static_cast<uint32_t>(lane & 7);
   int4* const slot0 = w32r_slot0 + 256 * wave;

@@ -157,7 +157,7 @@ def test_bench_gpus_n_launches_its_own_ranks(n):
     assert len(lines) == 1, r.stdout  # rank 0 only
     out = json.loads(lines[0])
     assert out["n_gpus"] == n and out["gpus_arg"] == n and out["max_rank"] == n - 1
-    assert out["ranks"] == [{"rank": i, "local_rank": i} for i in range(n)]
+    assert [(g["rank"], g["local_rank"]) for g in out["ranks"]] == [(i, i) for i in range(n)]
     assert out["ranks_launched_by"] == "bench.py"
 
 
@@ -180,3 +180,29 @@ def test_target_block():
     assert t["target_needs_frac_of_ceiling"] == pytest.approx(0.70 / 0.7071, abs=1e-3)
     t = bench.target_block(2147483648.0, 428.32)  # a mix whose best stream is below 0.70
     assert t["target_reachable"] is False and t["target_needs_frac_of_ceiling"] > 1
+
+
+def test_bench_launcher_stops_its_ranks_when_killed():
+    """SIGTERM to the launching bench.py (e.g. a driver timeout) reaches its ranks: none outlives it."""
+    import json
+    import signal
+    import subprocess
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rank-probe",
+                          "--probe-sleep", "60"], stdout=subprocess.PIPE, text=True, cwd=ROOT, env=env)
+    try:
+        line = p.stdout.readline()
+        pids = [g["pid"] for g in json.loads(line)["ranks"]]
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=30) == 128 + signal.SIGTERM
+        deadline = time.monotonic() + 20
+        alive = pids
+        while alive and time.monotonic() < deadline:
+            alive = [q for q in pids if os.path.exists(f"/proc/{q}") and
+                     open(f"/proc/{q}/stat").read().split()[2] != "Z"]
+            time.sleep(0.1)
+        assert not alive, f"ranks {alive} outlived the launcher"
+    finally:
+        if p.poll() is None:
+            p.kill()
