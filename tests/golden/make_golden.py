@@ -14,7 +14,8 @@ plain Python with the same dtypes.  Inputs follow the reference tests' generator
   * voltages:  np.random.default_rng(seed=2021).uniform(0, 255, shape).astype(np.uint8)
                (beamform_op_sequence_test.py:143-149, prebeamform_reorder_test.py:100-106)
   * delays:    (samples_delay*Ts, 0, phase, 0) for every (c, m, a) (beamform_coeff_test.py:86-90), plus
-               non-uniform random delays (this file) to pin the per-(c, m, a) index mapping.
+               non-uniform random delays (this file) to pin the per-(c, m, a) index mapping, plus (G5) delay models
+               with rates advanced to each batch's time exactly in float32 (the dt != 0 pin).
 
 Output: tests/golden/golden.npz (data only: inputs and the reference's outputs).
 """
@@ -140,6 +141,57 @@ xr = ref_reorder.reorder(raw, raw.shape, (B, 2, C, T // 16, 16, A, 2))
 y = complex_mult_cpu.complex_mult(xr, w, (B, 2, C, T // 16, 16, 2 * M))
 put("opseq_cfg1", dims=np.array([B, A, M, Ctot, T, C]), delays=d, input_sha256=sha(raw), output=y)
 print("opseq_cfg1", raw.shape, "->", y.shape)
+
+# ---- G5: the time extension (dt != 0) against the reference's own formula -----------------------------------
+# The Python reference reads only delay and phase (coeff_generator_cpu.py:125-164); a delay model with rates steers
+# batch b at dt_b = t0 + b * batch_dt as tau_b = tau + tau_rate * dt_b, phi_b = phi + phi_rate * dt_b.
+# The models here are built so that tau_b and phi_b are EXACT float32 numbers (tau on the 2^-51 grid inside
+# [2^-28, 2^-27), tau_rate * dt_b a multiple of 2^-51; phi on the 2^-23 grid inside [1, 2) or (-2, -1], phi_rate *
+# dt_b a multiple of 2^-23; t0 and batch_dt powers of two): the reference's cpu_coeffs on the advanced float32 model
+# (tau_b, 0, phi_b, 0) is then the time extension evaluated exactly, so the fused operator's coefficients at dt != 0
+# are pinned bit for bit by the reference's code, not by this framework's restatement.  Rates: up to ~2 sample
+# periods of delay drift and ~0.5 rad of phase drift over the batches (the convention -- which term each rate enters,
+# and its sign -- moves every coefficient).
+def exact_rate_model(M, A, seed, t0, batch_dt, nb):
+    rng = np.random.default_rng(seed)
+    d = np.empty((1, M, A, 4), np.float32)
+    tau_k = rng.integers(int(1.2 * 2 ** 23), int(1.8 * 2 ** 23), (M, A))          # tau = k 2^-51 in [2^-28, 2^-27)
+    tau_m = rng.integers(-2 ** 17, 2 ** 17, (M, A)) * 2                              # rate = m 2^-44
+    phi_k = rng.integers(int(1.1 * 2 ** 23), int(1.9 * 2 ** 23), (M, A)) * rng.choice([-1, 1], (M, A))
+    phi_n = rng.integers(-2 ** 15, 2 ** 15, (M, A))                                   # phase rate = n 2^-16
+    d[0, :, :, 0] = tau_k * 2.0 ** -51
+    d[0, :, :, 1] = tau_m * 2.0 ** -44
+    d[0, :, :, 2] = phi_k * 2.0 ** -23
+    d[0, :, :, 3] = phi_n * 2.0 ** -16
+    advanced = []
+    for b in range(nb):
+        dt = t0 + b * batch_dt
+        tau_b = d[0, :, :, 0].astype(np.float64) + d[0, :, :, 1].astype(np.float64) * dt
+        phi_b = d[0, :, :, 2].astype(np.float64) + d[0, :, :, 3].astype(np.float64) * dt
+        assert (tau_b.astype(np.float32) == tau_b).all() and (phi_b.astype(np.float32) == phi_b).all()
+        assert (np.abs(tau_b) >= 2.0 ** -28).all() and (np.abs(tau_b) < 2.0 ** -27).all()
+        assert (np.abs(phi_b) >= 1.0).all() and (np.abs(phi_b) < 2.0).all()
+        adv = np.zeros((M, A, 4), np.float32)
+        adv[..., 0] = tau_b
+        adv[..., 2] = phi_b
+        advanced.append(adv)
+    return d, advanced
+
+
+for name, (A, M, C, Ctot, xeng_id, nb) in {
+    "rates_a19_m2": (19, 2, 8, 1024, 3, 3),
+    "rates_a64_m16": (64, 16, 4, 4096, 5, 3),
+}.items():
+    t0, batch_dt = 2.0 ** -7, 2.0 ** -6
+    d, advanced = exact_rate_model(M, A, 500 + A, t0, batch_dt, nb)
+    w = np.empty((nb, C, 2 * A, 2 * M), np.float32)
+    for b, adv in enumerate(advanced):
+        wb = ref_coeffs(np.broadcast_to(adv, (C, M, A, 4)).copy(), 1, 2, C, Ctot, A, M, xeng_id)
+        w[b] = wb[0, 0]
+    drift = float(np.abs(w[-1] - w[0]).max())
+    assert drift > 0.1, drift  # the rates move the coefficients
+    put(name, dims=np.array([A, M, C, Ctot, xeng_id, nb]), times=np.array([t0, batch_dt]), delays=d, coeffs=w)
+    print(name, d.shape, "->", w.shape, "max drift over the batches", round(drift, 3))
 
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.npz")
 np.savez_compressed(path, **OUT)

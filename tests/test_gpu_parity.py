@@ -186,6 +186,46 @@ def test_coeff_gen_time_matches_oracle(context, command_queue):
         np.testing.assert_array_equal(got16[t, ..., 1], sin.transpose(0, 2, 1).astype(np.float16))
 
 
+@pytest.mark.parametrize("case", cases("rates_"))
+def test_coeff_gen_time_reference_golden(context, command_queue, case):
+    """dt != 0 pinned by the reference itself (G5, tests/golden/make_golden.py): delay models WITH rates whose
+    advanced delay and phase are exact float32 numbers at every batch time, so the reference's cpu_coeffs on the
+    advanced model is the time extension evaluated exactly.  The time generator's phasors equal it bit for bit."""
+    A, M, C, Ctot, xeng_id, nb = (int(v) for v in get(case, "dims"))
+    t0, bdt = (float(v) for v in get(case, "times"))
+    d = get(case, "delays")
+    w = get(case, "coeffs")  # (nb, C, 2A, 2M): W[2a][2m] = cos, W[2a][2m+1] = sin
+    dv = accel.DeviceArray(context, d.shape, np.float32)
+    dv.set(command_queue, d)
+    out = accel.DeviceArray(context, (nb, C, A, M, 2), np.float32)
+    _lib.call("bf_coeff_gen_time", dv.ptr, 1, out.ptr, 0, nb, C, Ctot, A, M, xeng_id, TS, t0, bdt,
+              command_queue.handle)
+    got = out.get(command_queue)
+    np.testing.assert_array_equal(got[..., 0], w[:, :, 0::2, 0::2])
+    np.testing.assert_array_equal(got[..., 1], w[:, :, 0::2, 1::2])
+
+
+@pytest.mark.parametrize("case", cases("rates_"))
+def test_fused_time_extension_reference_golden(context, command_queue, fused_path, case):
+    """The fused operator at dt != 0 (exact coefficients, per-batch regeneration from a model with rates) is the
+    reference's multiply applied to the reference's own per-batch tables (G5): identical bits to MatrixMultiply fed
+    the golden tables, on every fused kernel path."""
+    A, M, C, Ctot, xeng_id, B = (int(v) for v in get(case, "dims"))
+    t0, bdt = (float(v) for v in get(case, "times"))
+    T = 256
+    d = get(case, "delays")
+    w = np.ascontiguousarray(np.broadcast_to(get(case, "coeffs")[:, None], (B, 2, C, 2 * A, 2 * M)))
+    raw = O.u8_voltages((B, A, C, T, 2, 2), seed=A + M)
+    fu = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng_id, sample_period=TS, delay_channels=1,
+                                 t0=t0, batch_dt=bdt, exact_coeffs=True,
+                                 kernel_path=fused_path).instantiate(command_queue)
+    (y_fu,) = run(fu, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    mm = MatrixMultiplyTemplate(context, A, C, T, M, B).instantiate(command_queue)
+    (y_mm,) = run(mm, command_queue, {"inData": O.reorder(raw), "inCoeffs": w}, ["outData"])
+    np.testing.assert_array_equal(y_fu, y_mm)
+    assert_beams_allclose(y_fu, O.complex_mult(O.reorder(raw), w), O.reorder(raw), w)
+
+
 @pytest.mark.parametrize("shape", [(256, 64, 64, 16), (3, 6, 5, 3)])
 def test_coeff_gen_time_study_matches_study_golden(context, command_queue, shape):
     """The C++ study's own time-dependent convention (bf_coeff_gen_time_study, BeamformerKernels.cu:155-170) against

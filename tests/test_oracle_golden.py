@@ -63,6 +63,24 @@ def test_time_extension_at_zero_is_reference_phase():
     assert not np.array_equal(r0, r2)
 
 
+@pytest.mark.parametrize("case", cases("rates_"))
+def test_time_extension_golden(case):
+    """dt != 0 pinned by the reference (G5): the fused tables at dt_b = t0 + b*batch_dt, built from delay models WITH
+    rates, equal the reference's cpu_coeffs on the float32-exact advanced models (tau_b, 0, phi_b, 0) bit for bit."""
+    A, M, C, Ctot, xeng_id, nb = (int(v) for v in get(case, "dims"))
+    t0, batch_dt = (float(v) for v in get(case, "times"))
+    d = get(case, "delays")
+    assert d.shape == (1, M, A, 4) and (d[..., 1] != 0).all() and (d[..., 3] != 0).all()
+    w = O.fused_tables(d, nb, C, Ctot, A, xeng_id, O.TS_MEERKAT, t0, batch_dt)
+    for p in range(2):
+        np.testing.assert_array_equal(w[:, p], get(case, "coeffs"))
+    # and the rates matter: with them zeroed every batch's table is the dt = 0 table
+    d0 = d.copy()
+    d0[..., 1] = d0[..., 3] = 0
+    assert not np.array_equal(O.fused_tables(d0, nb, C, Ctot, A, xeng_id, O.TS_MEERKAT, t0, batch_dt)[:, 0],
+                              get(case, "coeffs"))
+
+
 def test_requantise_contract():
     y = np.array([0.5, 1.5, 2.5, -0.5, -1.5, 126.6, 1e9, -1e9, np.float32(127.49)], np.float32)
     np.testing.assert_array_equal(O.requantise(y, 1.0), [0, 2, 2, 0, -2, 127, 127, -127, 127])
