@@ -147,21 +147,9 @@ __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
   unsigned long long fix = 0;  // wave-uniform: bit j set when some lane left channel c0 + j undecided (nrun <= 64)
   uint32_t acc = 0;
   constexpr double kMagic = 0x1.8p52;
-  for (int j = 0; j < nrun; ++j) {
-    bool ok = in_range;
-    uint32_t word;
-    if (Gain || !P.unit_fast) {  // (uniform)
-      word = pack(q14_pair(re * 0x1p-14, gq, &ok), q14_pair(im * 0x1p-14, gq, &ok));
-    } else {
-      // t = 2^14 v: Q = rne(t) wherever t is farther than the margin from a half-integer (q14_pair_unit_scaled)
-      const double mc = re + kMagic, ms = im + kMagic;
-      int wc = static_cast<int>(static_cast<uint32_t>(__builtin_bit_cast(unsigned long long, mc)));
-      int ws = static_cast<int>(static_cast<uint32_t>(__builtin_bit_cast(unsigned long long, ms)));
-      if (!(fabs(re - (mc - kMagic)) < kQ14UnitMargin)) wc = q14_pair(re * 0x1p-14, 16384.0f, &ok);
-      if (!(fabs(im - (ms - kMagic)) < kQ14UnitMargin)) ws = q14_pair(im * 0x1p-14, 16384.0f, &ok);
-      word = pack(wc, ws);
-    }
-    if (__builtin_amdgcn_ballot_w64(ok) != __builtin_amdgcn_read_exec()) fix |= 1ull << j;
+  // a lane beyond the guard's range: every channel of the wave is evaluated exactly after the walk
+  if (__builtin_amdgcn_ballot_w64(!in_range)) fix = nrun >= 64 ? ~0ull : (1ull << nrun) - 1;
+  auto emit = [&](int j, uint32_t word) {  // store (or, diagnostics, fold) the word; step the recurrence
     if constexpr (Mode == 1)
       acc += word;
     else
@@ -169,6 +157,35 @@ __global__ __launch_bounds__(256) void q14_table_kernel(Q14TableArgs P) {
     const double r2 = fma(re, cd, -im * sd);
     im = fma(re, sd, im * cd);
     re = r2;
+  };
+  if (Gain || !P.unit_fast) {  // (uniform, hoisted out of the walk)
+    for (int j = 0; j < nrun; ++j) {
+      bool ok = true;
+      const uint32_t word = pack(q14_pair(re * 0x1p-14, gq, &ok), q14_pair(im * 0x1p-14, gq, &ok));
+      if (__builtin_amdgcn_ballot_w64(ok) != __builtin_amdgcn_read_exec()) fix |= 1ull << j;
+      emit(j, word);
+    }
+  } else {
+    // t = 2^14 v: Q = rne(t) wherever t is farther than the margin from a half-integer (q14_pair_unit_scaled).  The
+    // ~0.2 % of components nearer a boundary (some lane in ~1 of 4 wave-channels) take q14_pair's two-sided test
+    // under ONE wave-uniform branch, and only that branch tracks undecided lanes: the common path is the recurrence,
+    // four float64 margin operations per component, a v_perm and the store (round 6: the walk's scalar work --
+    // two exec-mask branches and the per-channel flag update -- was ~18 SALU per channel against ~22 VALU,
+    // profiles/r6_l_cfg4_gen_pmc.txt).
+    for (int j = 0; j < nrun; ++j) {
+      const double mc = re + kMagic, ms = im + kMagic;
+      int wc = static_cast<int>(static_cast<uint32_t>(__builtin_bit_cast(unsigned long long, mc)));
+      int ws = static_cast<int>(static_cast<uint32_t>(__builtin_bit_cast(unsigned long long, ms)));
+      const bool uc = !(fabs(re - (mc - kMagic)) < kQ14UnitMargin);
+      const bool us = !(fabs(im - (ms - kMagic)) < kQ14UnitMargin);
+      if (__builtin_amdgcn_ballot_w64(uc || us)) {
+        bool ok = true;
+        if (uc) wc = q14_pair(re * 0x1p-14, 16384.0f, &ok);
+        if (us) ws = q14_pair(im * 0x1p-14, 16384.0f, &ok);
+        if (__builtin_amdgcn_ballot_w64(ok) != __builtin_amdgcn_read_exec()) fix |= 1ull << j;
+      }
+      emit(j, pack(wc, ws));
+    }
   }
   if constexpr (Mode == 1) {
     if (acc == 0x9e3779b9u) *o = acc;
