@@ -193,6 +193,21 @@ for name, (A, M, C, Ctot, xeng_id, nb) in {
     put(name, dims=np.array([A, M, C, Ctot, xeng_id, nb]), times=np.array([t0, batch_dt]), delays=d, coeffs=w)
     print(name, d.shape, "->", w.shape, "max drift over the batches", round(drift, 3))
 
+# G5 at config 4's shape (A = 256, M = 64: the int8 path's Q14 generator and LDS-DMA contraction).  The float table
+# would be 1.5 MB per channel pair; the int8 contract only needs its Q14 image, W = rne(2^14 w) of the reference's
+# float32 coefficient (oracle.quantise_coeffs), stored as int16 (Wc, Ws) per (batch, channel, beam, antenna).
+for name, (A, M, C, Ctot, xeng_id, nb) in {"q14rates_a256_m64": (256, 64, 2, 32768, 5, 3)}.items():
+    t0, batch_dt = 2.0 ** -7, 2.0 ** -6
+    d, advanced = exact_rate_model(M, A, 700 + A, t0, batch_dt, nb)
+    q = np.empty((nb, C, M, A, 2), np.int16)
+    for b, adv in enumerate(advanced):
+        wb = ref_coeffs(np.broadcast_to(adv, (C, M, A, 4)).copy(), 1, 2, C, Ctot, A, M, xeng_id)[0, 0]
+        qb = np.rint(wb.astype(np.float64) * 16384.0).astype(np.int64)  # (C, 2A, 2M)
+        q[b, ..., 0] = qb[:, 0::2, 0::2].transpose(0, 2, 1)  # Wc: W[2a][2m]
+        q[b, ..., 1] = qb[:, 0::2, 1::2].transpose(0, 2, 1)  # Ws: W[2a][2m + 1]
+    put(name, dims=np.array([A, M, C, Ctot, xeng_id, nb]), times=np.array([t0, batch_dt]), delays=d, q14=q)
+    print(name, d.shape, "->", q.shape)
+
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.npz")
 np.savez_compressed(path, **OUT)
 print("wrote", path, os.path.getsize(path), "bytes; sha256",

@@ -226,6 +226,33 @@ def test_fused_time_extension_reference_golden(context, command_queue, fused_pat
     assert_beams_allclose(y_fu, O.complex_mult(O.reorder(raw), w), O.reorder(raw), w)
 
 
+@pytest.mark.parametrize("case", cases("rates_"))
+@pytest.mark.parametrize("signed", [True, False])
+@pytest.mark.parametrize("i8_kernel", ["auto", "item", "generic", "wide", "wide-inkernel"])
+def test_fused_int8_time_extension_reference_golden(context, command_queue, i8_kernel, signed, case):
+    """The int8 (requantised) beams at dt != 0 from the reference's own per-batch tables (G5): W = rne(2^14 w) of the
+    golden float32 coefficients, exact integer products, one rounding to int8 -- bit for bit on every int8 kernel
+    path, the in-kernel phasor path included."""
+    A, M, C, Ctot, xeng_id, B = (int(v) for v in get(case, "dims"))
+    t0, bdt = (float(v) for v in get(case, "times"))
+    T, scale = 256, 1.0 / 64
+    d = get(case, "delays")
+    W = O.quantise_coeffs(np.broadcast_to(get(case, "coeffs")[:, None], (B, 2, C, 2 * A, 2 * M)))
+    rng = np.random.default_rng(A * 5 + M)
+    raw = rng.integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8)
+    if signed:
+        raw = raw.view(np.int8)
+    op = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng_id, sample_period=TS, delay_channels=1,
+                                 sample_signed=signed, out_int8=True, out_scale=scale, t0=t0, batch_dt=bdt,
+                                 **i8_path(i8_kernel)).instantiate(command_queue)
+    (q,) = run(op, command_queue, {"inSamples": raw, "delay_vals": d}, ["outData"])
+    xr = O.reorder(raw)
+    X = (xr.view(np.int8) if signed else xr).astype(np.int64).reshape(B, 2, C, T, 2 * A)
+    s = np.float32(np.float32(scale) * np.float32(2.0 ** -14))
+    ref = np.clip(np.rint(np.matmul(X, W).astype(np.float32) * s), -127, 127).astype(np.int8)
+    np.testing.assert_array_equal(q, ref.reshape(q.shape))
+
+
 @pytest.mark.parametrize("shape", [(256, 64, 64, 16), (3, 6, 5, 3)])
 def test_coeff_gen_time_study_matches_study_golden(context, command_queue, shape):
     """The C++ study's own time-dependent convention (bf_coeff_gen_time_study, BeamformerKernels.cu:155-170) against

@@ -13,6 +13,7 @@ import pytest
 import oracle as O
 from dpdk_dc_sand_amd import _lib, accel
 from dpdk_dc_sand_amd.beamforming import FusedBeamformerTemplate
+from golden_io import get
 
 pytestmark = pytest.mark.gpu
 TS = O.TS_MEERKAT
@@ -128,6 +129,51 @@ def test_fused_int8_table_path_equals_in_kernel_and_oracle(context, command_queu
     np.testing.assert_array_equal(outs[True], outs[False])
     ref = O.fused_beamform_int8(raw, d, Ctot, xeng_id=xeng, t0=t0, batch_dt=bdt, scale=1 / 64, signed=signed, gains=g)
     np.testing.assert_array_equal(outs[True], ref)
+    assert np.abs(ref.astype(int)).max() >= 8
+
+
+def golden_q14_words(case="q14rates_a256_m64"):
+    """The reference-pinned Q14 image of golden G5 at config 4's shape: (B, C, M, A) words Wc | Ws << 16."""
+    q = get(case, "q14").astype(np.int64)
+    return ((q[..., 0] & 0xffff) | ((q[..., 1] & 0xffff) << 16)).astype(np.uint32)
+
+
+def test_q14_coeffs_reference_golden_at_config4_shape(context, command_queue):
+    """dt != 0 at config 4's shape (A = 256, M = 64, Ctot = 32768, X-engine 5, three batches) pinned by the reference
+    (G5, tests/golden/make_golden.py): a delay model with rates whose advanced delay and phase are exact float32
+    numbers at each batch time, so the reference's cpu_coeffs on the advanced model is the time extension evaluated
+    exactly.  The generator's words equal rne(2^14 w) of those coefficients."""
+    A, M, C, Ctot, xeng, B = (int(v) for v in get("q14rates_a256_m64", "dims"))
+    t0, bdt = (float(v) for v in get("q14rates_a256_m64", "times"))
+    got = generate(context, command_queue, get("q14rates_a256_m64", "delays"), B, C, Ctot, A, M, xeng, t0, bdt)
+    np.testing.assert_array_equal(got, golden_q14_words())
+
+
+@pytest.mark.parametrize("table", [True, False])
+def test_fused_int8_config4_shape_reference_golden(context, command_queue, table):
+    """The cfg4 int8 beams at dt != 0 -- the Q14 generator + LDS-DMA ring contraction (table) and the in-kernel
+    phasor kernel -- from the reference's own coefficients (G5): exact integer products of Q14(golden), one rounding."""
+    A, M, C, Ctot, xeng, B = (int(v) for v in get("q14rates_a256_m64", "dims"))
+    t0, bdt = (float(v) for v in get("q14rates_a256_m64", "times"))
+    T, scale = 256, 1.0 / 64
+    raw = np.random.default_rng(11).integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8).view(np.int8)
+    tmpl = FusedBeamformerTemplate(context, B, C, Ctot, T, A, M, xeng_id=xeng, delay_channels=1, sample_signed=True,
+                                   out_int8=True, out_scale=scale, t0=t0, batch_dt=bdt, coeff_table=table)
+    assert (tmpl.workspace_bytes > 0) == table
+    op = tmpl.instantiate(command_queue)
+    op.ensure_all_bound()
+    op.buffer("inSamples").set(command_queue, raw)
+    op.buffer("delay_vals").set(command_queue, get("q14rates_a256_m64", "delays"))
+    op()
+    q = op.buffer("outData").get(command_queue)
+    g = get("q14rates_a256_m64", "q14").astype(np.int64)  # (B, C, M, A, [Wc, Ws])
+    W = np.empty((B, C, 2 * A, 2 * M), np.int64)  # [[Wc, Ws], [-Ws, Wc]] blocks (coeff_generator_cpu.py:170-186)
+    wc, ws = g[..., 0].transpose(0, 1, 3, 2), g[..., 1].transpose(0, 1, 3, 2)
+    W[:, :, 0::2, 0::2], W[:, :, 0::2, 1::2], W[:, :, 1::2, 0::2], W[:, :, 1::2, 1::2] = wc, ws, -ws, wc
+    X = O.reorder(raw).view(np.int8).astype(np.int64).reshape(B, 2, C, T, 2 * A)
+    s = np.float32(np.float32(scale) * np.float32(2.0 ** -14))
+    ref = np.clip(np.rint(np.matmul(X, W[:, None]).astype(np.float32) * s), -127, 127).astype(np.int8)
+    np.testing.assert_array_equal(q, ref.reshape(q.shape))
     assert np.abs(ref.astype(int)).max() >= 8
 
 

@@ -81,6 +81,35 @@ def test_time_extension_golden(case):
                               get(case, "coeffs"))
 
 
+@pytest.mark.parametrize("case", cases("rates_"))
+def test_int8_time_extension_golden(case):
+    """The int8 contract at dt != 0 (oracle.fused_beamform_int8 on a model with rates) from the reference's own
+    per-batch tables (G5): Q14 of the golden coefficients, exact integer products, one rounding."""
+    A, M, C, Ctot, xeng_id, B = (int(v) for v in get(case, "dims"))
+    t0, bdt = (float(v) for v in get(case, "times"))
+    T, scale = 32, 1.0 / 16
+    raw = np.random.default_rng(A).integers(0, 256, (B, A, C, T, 2, 2), dtype=np.uint8).view(np.int8)
+    q = O.fused_beamform_int8(raw, get(case, "delays"), Ctot, xeng_id=xeng_id, t0=t0, batch_dt=bdt, scale=scale,
+                              signed=True)
+    W = O.quantise_coeffs(np.broadcast_to(get(case, "coeffs")[:, None], (B, 2, C, 2 * A, 2 * M)))
+    X = O.reorder(raw).view(np.int8).astype(np.int64).reshape(B, 2, C, T, 2 * A)
+    s = np.float32(np.float32(scale) * np.float32(2.0 ** -14))
+    ref = np.clip(np.rint(np.matmul(X, W).astype(np.float32) * s), -127, 127).astype(np.int8)
+    np.testing.assert_array_equal(q, ref.reshape(q.shape))
+
+
+def test_q14_time_extension_golden_at_config4_shape():
+    """G5 at config 4's shape: the int8 contract's Q14 coefficients of the oracle (quantise_coeffs of fused_tables,
+    a model with rates at dt_b = t0 + b batch_dt) equal rne(2^14 w) of the reference's coefficients."""
+    A, M, C, Ctot, xeng, B = (int(v) for v in get("q14rates_a256_m64", "dims"))
+    t0, bdt = (float(v) for v in get("q14rates_a256_m64", "times"))
+    w = O.quantise_coeffs(O.fused_tables(get("q14rates_a256_m64", "delays"), B, C, Ctot, A, xeng, O.TS_MEERKAT, t0,
+                                         bdt))
+    q = get("q14rates_a256_m64", "q14")
+    np.testing.assert_array_equal(w[:, 0, :, 0::2, 0::2].transpose(0, 1, 3, 2), q[..., 0])
+    np.testing.assert_array_equal(w[:, 0, :, 0::2, 1::2].transpose(0, 1, 3, 2), q[..., 1])
+
+
 def test_requantise_contract():
     y = np.array([0.5, 1.5, 2.5, -0.5, -1.5, 126.6, 1e9, -1e9, np.float32(127.49)], np.float32)
     np.testing.assert_array_equal(O.requantise(y, 1.0), [0, 2, 2, 0, -2, 127, 127, -127, 127])
