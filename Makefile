@@ -7,7 +7,7 @@ LIB      := dpdk_dc_sand_amd/libbf.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -munsafe-fp-atomics
 SRCS     := $(CSRC)/bf_runtime.cpp $(CSRC)/bf_coeff.hip $(CSRC)/bf_reorder.hip $(CSRC)/bf_beamform.hip \
             $(CSRC)/bf_fused.hip $(CSRC)/bf_wide.hip $(CSRC)/bf_wide_i8.hip $(CSRC)/bf_q14table.hip $(CSRC)/bf_requant.hip \
-            $(CSRC)/bf_pipeline.cpp $(CSRC)/bf_comm.cpp
+            $(CSRC)/bf_study.hip $(CSRC)/bf_pipeline.cpp $(CSRC)/bf_comm.cpp
 OBJS     := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 HDRS     := $(wildcard $(CSRC)/*.hpp) $(wildcard $(CSRC)/diag/*.inc) include/bf.h
 

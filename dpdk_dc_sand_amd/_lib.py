@@ -51,6 +51,8 @@ PROTOTYPES = {
                                   c_double, c_double, c_double, c_void_p]),
     "bf_coeff_gen_time_study": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
                                         c_void_p]),
+    "bf_beamform_study_single_channel": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                                                 c_int, c_void_p]),
     "bf_reorder": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "bf_beamform": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_void_p]),

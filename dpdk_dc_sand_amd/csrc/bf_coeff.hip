@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void coeff_gen_time_study_kernel(const float4*
     const float delta_time = t * ts * fft_size;
     const float delta_delay = d.y * delta_time;
     const float delta_phase = d.w * delta_time;
-    const float delay_n2 = (d.x + delta_delay) * (C / 2) * pi / (ts * C);
+    const float delay_n2 = (d.x + delta_delay) * (static_cast<float>(C) / 2.0f) * pi / (ts * C);  // C / 2.0f: odd C too
     const float delay_n = (d.y + delta_delay) * c * pi / (ts * C);
     const float phase0 = d.z - delay_n2 + delta_phase;
     const float rotation = delay_n + phase0;

@@ -103,7 +103,7 @@ const char* bf_last_error(void) { return bf::g_last_error.c_str(); }
 
 // 3.0: 0x0500 (BF_FUSED_PATH_WIDE16), accepted by 2.0, is rejected; bf_coeff_gen_time_study, bf_comm_stats,
 // bf_comm_load and bf_checksum added; the root's own scatter slice is a 2-D copy at N > 1 (include/bf.h).
-int bf_abi_version(void) { return 301; }
+int bf_abi_version(void) { return 302; }
 
 int bf_device_count(int* count) {
   BF_REQUIRE(count != nullptr, "bf_device_count: null pointer");

@@ -34,7 +34,8 @@ extern "C" {
 const char* bf_last_error(void);
 /* ABI version: major * 100 + minor.  300: ABI 3.0 -- 0x0500 (BF_FUSED_PATH_WIDE16, accepted by 2.0) is rejected as an
  * unknown path, and bf_coeff_gen_time_study, bf_comm_stats, bf_comm_load and bf_checksum were added.  301: ABI 3.1 --
- * bf_scatter_plan added (the channel scatter's operation list as a pure host function). */
+ * bf_scatter_plan added (the channel scatter's operation list as a pure host function).  302: ABI 3.2 --
+ * bf_beamform_study_single_channel added (the C++ study's fused kernel in its own semantics). */
 int bf_abi_version(void);
 
 /* ---- runtime helpers (device memory, streams, events) -------------------------------------------------
@@ -102,6 +103,18 @@ int bf_coeff_gen_time(const float* delay_vals, int delay_channels, void* out, in
  *   out        : (n_times, C, A, M) complex: out_fp16 = 0 -> float2 (cos, sin); 1 -> half2 */
 int bf_coeff_gen_time_study(const float* delay_vals, void* out, int out_fp16, int n_times, int C, int A, int M,
                             float sample_period, int fft_size, void* stream);
+
+/* The C++ study's fused coefficient + beamform kernel in the study's OWN semantics (replaces
+ * calculate_beamweights_and_beamform_single_channel, BeamformerKernels.cu:192-367, as its harness's golden checks it,
+ * BeamformerCoefficientTest.cu:356-400): per channel c, time t and beam m
+ *   y_re = sum_a cos(rot) x_re,  y_im = sum_a sin(rot) x_im    (NOT a complex product: the study's semantics)
+ * with rot bf_coeff_gen_time_study's expression at (t, c, a, m), antennas summed in order in float32.  The kernel's
+ * shadowed prefetch (:277-282: every chunk after the first re-uses the first chunk's voltages) is not reproduced.
+ *   delay_vals : f32 (M*A, 4), index m*A + a (the combined kernel's beam-major order)
+ *   x          : int8 [C][T/16][A][16][2]  (char2 [channels][time/16][station][16]);  T % 16 == 0, A <= 2048
+ *   out        : f32  [C][T/16][M][16][2] */
+int bf_beamform_study_single_channel(const float* delay_vals, const int8_t* x, float* out, int C, int T, int A, int M,
+                                     float sample_period, int fft_size, void* stream);
 
 /* Pre-beamform reorder, bit-exact.
  * Replaces PreBeamformReorder._run / prebeamform_reorder kernel (beamformer/beamforming/prebeamform_reorder.py:

@@ -239,3 +239,25 @@ def study_coeffs_time(delay_vals, n_times, C, A, M, Ts=STUDY_TS, fft_size=STUDY_
     phase0 = ((phase - delay_n2) + dphase).astype(np.float32)
     rot = (delay_n + phase0).astype(np.float32).astype(np.float64)
     return (np.cos(rot).astype(np.float32) + 1j * np.sin(rot).astype(np.float32)).astype(np.complex64)
+
+
+def study_beams_single_channel(delay_vals, x, C, T, A, M, Ts=STUDY_TS, fft_size=STUDY_FFT):
+    """The study harness's golden for its fused kernel (BeamformerCoeffTest::verify_output, the
+    COMBINED_COEFF_GEN_AND_BEAMFORMER_SINGLE_CHANNEL case, BeamformerCoefficientTest.cu:356-400):
+        y_re[c][t_ex][b][t_in] = sum_a cos(rot) * x_re,   y_im = sum_a sin(rot) * x_im        (:385-394)
+    -- the study's own semantics, not a complex product -- with the coefficients of study_coeffs_time at
+    time t = 16 t_ex + t_in and the delay model of (a, b) at index b*A + a (the combined kernel's ordering, :307-316).
+    Each product and each partial sum is one float32 rounding, antennas in order, as the golden's loop.
+    delay_vals: (M*A, 4) float32; x: int8 (C, T/16, A, 16, 2).  Returns float32 (C, T/16, M, 16, 2)."""
+    d = np.asarray(delay_vals, np.float32).reshape(M, A, 4).transpose(1, 0, 2).reshape(A * M, 4)
+    w = study_coeffs_time(d, T, C, A, M, Ts, fft_size)  # (T, C, A, M)
+    w = w.reshape(T // 16, 16, C, A, M).transpose(2, 0, 3, 4, 1)  # (C, T/16, A, M, 16)
+    cs, sn = np.ascontiguousarray(w.real), np.ascontiguousarray(w.imag)
+    xv = np.asarray(x, np.int8).reshape(C, T // 16, A, 16, 2).astype(np.float32)
+    re = np.zeros((C, T // 16, M, 16), np.float32)
+    im = np.zeros((C, T // 16, M, 16), np.float32)
+    for a in range(A):
+        re += cs[:, :, a] * xv[:, :, a, None, :, 0]
+        im += sn[:, :, a] * xv[:, :, a, None, :, 1]
+    return np.stack([re, im], axis=-1)
+

@@ -42,7 +42,7 @@ def test_prototypes_match_header():
 
 def test_abi_version_and_error_channel():
     lib = _lib.load()
-    assert lib.bf_abi_version() == 301  # 3.1: bf_scatter_plan added to 3.0 (WIDE16 (0x500) rejected)
+    assert lib.bf_abi_version() == 302  # 3.2: bf_beamform_study_single_channel; 3.1: bf_scatter_plan (WIDE16 rejected)
     assert isinstance(_lib.last_error(), str)
 
 
@@ -68,6 +68,14 @@ def test_argument_validation_without_gpu():
         _lib.call("bf_coeff_gen_time_study", fake, fake, 0, 4, 4, 4, 4, 0.0, 8192, None)
     with pytest.raises(_lib.BeamformerError, match="misaligned"):
         _lib.call("bf_coeff_gen_time_study", fake + 4, fake, 0, 4, 4, 4, 4, 1e-7, 8192, None)
+    with pytest.raises(_lib.BeamformerError, match="null pointer"):
+        _lib.call("bf_beamform_study_single_channel", fake, None, fake, 4, 32, 4, 4, 1e-7, 8192, None)
+    with pytest.raises(_lib.BeamformerError, match="multiple of 16"):
+        _lib.call("bf_beamform_study_single_channel", fake, fake, fake, 4, 40, 4, 4, 1e-7, 8192, None)
+    with pytest.raises(_lib.BeamformerError, match="above 2048"):
+        _lib.call("bf_beamform_study_single_channel", fake, fake, fake, 4, 32, 4096, 4, 1e-7, 8192, None)
+    with pytest.raises(_lib.BeamformerError, match="misaligned"):
+        _lib.call("bf_beamform_study_single_channel", fake + 4, fake, fake, 4, 32, 4, 4, 1e-7, 8192, None)
 
 
 def test_algorithmic_bytes():

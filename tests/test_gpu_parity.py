@@ -253,7 +253,7 @@ def test_fused_int8_time_extension_reference_golden(context, command_queue, i8_k
     np.testing.assert_array_equal(q, ref.reshape(q.shape))
 
 
-@pytest.mark.parametrize("shape", [(256, 64, 64, 16), (3, 6, 5, 3)])
+@pytest.mark.parametrize("shape", [(256, 64, 64, 16), (3, 6, 5, 3), (4, 7, 5, 3)])
 def test_coeff_gen_time_study_matches_study_golden(context, command_queue, shape):
     """The C++ study's own time-dependent convention (bf_coeff_gen_time_study, BeamformerKernels.cu:155-170) against
     its harness's golden (BeamformerCoefficientTest.cu:294-337, restated in oracle.study_coeffs_time) on the
@@ -280,6 +280,45 @@ def test_coeff_gen_time_study_matches_study_golden(context, command_queue, shape
     # the rates matter at the study's shape: its last time's phasors are far from its first's
     if NT >= 256:
         assert np.abs(ref[-1] - ref[0]).max() > 0.5
+
+
+@pytest.mark.parametrize("shape,inputs", [((64, 256, 64, 16), "harness"), ((5, 48, 37, 20), "random")])
+def test_study_single_channel_beamformer_matches_study_golden(context, command_queue, shape, inputs):
+    """The C++ study's fused kernel in its own semantics (bf_beamform_study_single_channel; replaces
+    calculate_beamweights_and_beamform_single_channel, BeamformerKernels.cu:192-367) against its harness's golden
+    (BeamformerCoefficientTest.cu:356-400, restated in oracle.study_beams_single_channel): y_re = sum_a cos x_re,
+    y_im = sum_a sin x_im per (channel, time, beam), the study's time-dependent phasor per sample.  At the study's
+    default shape on the harness's own inputs (simulate_input: delay ramp, x[i] = (int8) i), and at a ragged shape
+    (odd channel count, more beams than a workgroup's 16 beam slots, random int8 samples and delay model with rates).
+    Bars: the harness's own, 1e-1 absolute on every beam (runBeamformerTests.cpp:14); and a float32 one, 2e-5 of
+    sum_a |x| -- the phasors' argument carries the study's float32 rounding (|rot| up to ~60 rad: ulp 4e-6) and the
+    kernel's dt = t Ts fft against the golden's truncated nanoseconds."""
+    C, T, A, M = shape
+    if inputs == "harness":
+        d = O.study_delay_ramp(A, M)
+        x = np.arange(C * T * A * 2, dtype=np.int64).astype(np.int8).reshape(C, T // 16, A, 16, 2)
+    else:
+        rng = np.random.default_rng(C * T + A)
+        d = np.zeros((M * A, 4), np.float32)
+        d[:, 0] = rng.uniform(0, 1e-7 / 3, M * A)
+        d[:, 1] = rng.uniform(-3e-6, 3e-6, M * A)
+        d[:, 2] = rng.uniform(-np.pi, np.pi, M * A)
+        d[:, 3] = rng.uniform(-1e-5, 1e-5, M * A)
+        x = rng.integers(-128, 128, (C, T // 16, A, 16, 2), dtype=np.int64).astype(np.int8)
+    dv = accel.DeviceArray(context, d.shape, np.float32)
+    dv.set(command_queue, d)
+    xv = accel.DeviceArray(context, x.shape, np.int8)
+    xv.set(command_queue, x)
+    out = accel.DeviceArray(context, (C, T // 16, M, 16, 2), np.float32)
+    _lib.call("bf_beamform_study_single_channel", dv.ptr, xv.ptr, out.ptr, C, T, A, M, ctypes.c_float(1e-7), 8192,
+              command_queue.handle)
+    y = out.get(command_queue)
+    ref = O.study_beams_single_channel(d, x, C, T, A, M)
+    err = np.abs(y.astype(np.float64) - ref)
+    assert err.max() <= 1e-1  # the harness's tolerance for this kernel (runBeamformerTests.cpp:14)
+    mag = np.abs(x.astype(np.float64)).sum(axis=2).transpose(0, 1, 2, 3)[:, :, None]  # (C, T/16, 1, 16, 2)
+    assert (err <= 2e-5 * mag + 1e-6).all(), float((err / (2e-5 * mag + 1e-6)).max())
+    assert np.abs(ref).max() > 100  # the beams are far from zero
 
 
 # ---- beamform multiply (beamform_mult_kernel_test.py:119-269: rtol = atol = 1e-4) -------------------------

@@ -221,3 +221,29 @@ def test_study_time_golden_restatement():
     assert np.allclose(np.angle(w[0, 0, :, :]).ravel(),
                        np.angle(np.exp(1j * (d[:, 2].astype(np.float64) - d[:, 0] * (C / 2) * np.pi / (1e-7 * C)))),
                        atol=1e-6)
+
+
+def test_study_single_channel_beams_restatement():
+    """oracle.study_beams_single_channel (the study harness's golden for its fused kernel, BeamformerCoefficientTest.cu:
+    356-400, vectorised over channels, chunks and beams) equals the golden's own loop nest restated literally -- per
+    (c, t_ex, b, t_in) a float32 sum over the antennas in order of cos(rot) x_re and sin(rot) x_im (the study's
+    non-complex product) with the coefficient of delay entry b*A + a -- on the harness's inputs
+    (simulate_input, :185-204: the delay ramp and x[i] = (int8) i)."""
+    f32 = np.float32
+    C, T, A, M = 6, 32, 5, 3
+    d = O.study_delay_ramp(A, M)
+    x = np.arange(C * T * A * 2, dtype=np.int64).astype(np.int8).reshape(C, T // 16, A, 16, 2)
+    y = O.study_beams_single_channel(d, x, C, T, A, M)
+    assert y.shape == (C, T // 16, M, 16, 2) and y.dtype == np.float32
+    w = O.study_coeffs_time(d.reshape(M, A, 4).transpose(1, 0, 2).reshape(A * M, 4), T, C, A, M)  # index a*M + b
+    for c, tex, b, tin in ((0, 0, 0, 0), (5, 1, 2, 15), (3, 0, 1, 7), (1, 1, 0, 9)):
+        re = im = f32(0)
+        for a in range(A):
+            co = w[16 * tex + tin, c, a, b]
+            re = f32(re + f32(co.real * f32(x[c, tex, a, tin, 0])))
+            im = f32(im + f32(co.imag * f32(x[c, tex, a, tin, 1])))
+        assert y[c, tex, b, tin, 0] == re and y[c, tex, b, tin, 1] == im, (c, tex, b, tin)
+    # not a complex product: the real beam ignores x_im entirely
+    x2 = x.copy()
+    x2[..., 1] = 0
+    np.testing.assert_array_equal(O.study_beams_single_channel(d, x2, C, T, A, M)[..., 0], y[..., 0])

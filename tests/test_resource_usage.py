@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "dpdk_dc_sand_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 SOURCES = ["bf_coeff.hip", "bf_reorder.hip", "bf_beamform.hip", "bf_fused.hip", "bf_wide.hip", "bf_wide_i8.hip",
-           "bf_q14table.hip", "bf_requant.hip"]
+           "bf_q14table.hip", "bf_requant.hip", "bf_study.hip"]
 
 
 def _usage(src):
